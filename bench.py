@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GoL cell updates/s (GCUPS) on MI355X.
+
+Workload (BASELINE.json configs[3], the metric's headline size): one 65536 x 65536
+random torus board (seed 3, oracle/bitref.c generator), `--steps` turns timed
+after `--warmup` untimed turns.  One step = one turn = one pass of the per-turn
+board update (reference calculateNextState, SubServer/distributor.go:119-208)
+over the whole board.  The board is resident in HBM (bit-packed, 512 MiB per
+buffer) before the timed region; no PGM I/O or alive-list work is timed.
+
+N = 1: one torus engine.  N > 1 (torchrun, one rank per GPU): the board's rows
+are split as the reference Server splits them (Server/gol/distributor.go:106-116)
+and each rank exchanges `--halo` boundary rows with its ring neighbours over
+RCCL every `--halo` turns ("strong" scaling: the total board is fixed).
+
+Printed (rank 0): one JSON line with the driver's contract fields plus
+`roofline` (k_step_fast: algorithmic 0.25 B per cell-update vs 8 TB/s HBM) and
+`cpu_baseline` (oracle/refcpu.c, the C restatement of the reference's CPU path,
+timed on a bounded sample on this host).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "conway-s-gol-distributed_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "cell updates/sec (GCUPS) at 16384² & 65536², 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_CELL_UPDATE = 0.25   # 1 bit read + 1 bit written per cell per turn
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--size", type=int, default=65536, help="board side (default 65536)")
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--halo", type=int, default=32, help="strip halo depth K (N > 1)")
+    ap.add_argument("--band", type=int, default=0, help="stencil band rows (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-turns", type=int, default=2)
+    ap.add_argument("--cpu-cores", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(size, seed, turns, cores):
+    """oracle/refcpu.c (literal restatement of the reference's Server/SubServer CPU path,
+    4 sub-servers as in the reference's default SUB list, Threads = cores) on the same
+    board for a bounded number of turns."""
+    from oracle import oracle as O
+    board = O.unpack(O.gen_random(seed, size, size), size)
+    t0 = time.perf_counter()
+    O.ref_run(board, turns, nsub=4, threads=cores, ncores=cores)
+    dt = time.perf_counter() - t0
+    del board
+    return {"value": round(size * size * turns / dt / 1e9, 4), "unit": "GCUPS",
+            "cores": cores, "kind": "port",
+            "sample": f"{size}x{size} random board seed {seed}, {turns} turns, oracle/refcpu.c "
+                      f"(4 sub-servers x {cores} threads, no gob/HTTP: optimistic), {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import gol
+    from gol.distributed import DistStrip, EngineStrip, make_engine_strip
+
+    W = H = a.size
+    stream = torch.cuda.current_stream(dev)
+    if world == 1:
+        eng = gol.Engine(W, H, device=local, band_rows=a.band)
+        eng.set_stream(stream.cuda_stream)
+        eng.fill_random(a.seed)
+        runner = eng
+        rows_local = H
+    else:
+        eng = make_engine_strip(W, H, rank, world, a.halo, local, band_rows=a.band)
+        eng.set_stream(stream.cuda_stream)
+        eng.fill_random(a.seed)
+        runner = DistStrip(EngineStrip(eng, dev), rank, world)
+        rows_local = eng.rows
+    info = eng.info()
+
+    runner.step(a.warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+    torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    runner.step(a.steps)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    # per-launch average of the stencil on this rank's stream (one launch per turn)
+    cells_local = rows_local * W
+    launch_us = gpu_ms * 1e3 / a.steps
+    achieved = BYTES_PER_CELL_UPDATE * cells_local / (launch_us * 1e-6) / 1e9
+    gcups = W * H * a.steps / wall / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(gcups, 2),
+            "unit": "GCUPS",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(wall * 1e3 / a.steps, 5),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": f"{W}x{H} random torus board (seed {a.seed}), "
+                                   f"{a.steps} turns, bit-packed k=1 stencil",
+                       "board": [W, H], "turns": a.steps,
+                       "parallelism": f"row-strips x{world}" + (f", halo {info.halo}" if world > 1 else ""),
+                       "band_rows": info.band_rows, "fast_path": bool(info.fast_path),
+                       "temporal_blocking_k": 1},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "k_step_fast",
+                         "launch_us": round(launch_us, 2),
+                         "bytes_per_launch": int(BYTES_PER_CELL_UPDATE * cells_local)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(W, a.seed, a.cpu_turns, a.cpu_cores)
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,697 @@
+// gol_engine.cpp — the per-GPU engine behind include/gol_amd.h.
+//
+// One gol_ctx = one MI355X holding either the whole torus board or one row
+// strip of it (the reference's SubServer strip, Server/gol/distributor.go:
+// 106-116 split; here the strip lives on the GPU for the whole run and only
+// `halo` boundary rows move between strips every `halo` turns).
+//
+// Device memory per engine (owned here, freed in gol_destroy):
+//   board[2]   double-buffered packed board, buffer_rows x pitch uint64
+//   blocked    packed mask of the cells that were neither 0 nor 255 at load
+//              (only while turn 1 is pending; reference quirk,
+//              SubServer/distributor.go:178-200 + :122-125)
+//   counts     popcount shards (kShards u64) x kRing slots for the per-turn
+//              series (GOL_FLAG_COUNT_EVERY_TURN) and one slot for snapshots
+//   staging    byte / alive-list staging, allocated on demand
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gol_amd.h"
+#include "gol_kernels.h"
+#include "gol_internal.h"
+
+using golk::kShards;
+
+namespace {
+
+constexpr int kRing = 4096;                 // per-turn count ring (turn t -> slot t % kRing)
+constexpr size_t kStagingBytes = 256u << 20;  // byte staging chunk for load / read
+
+}  // namespace
+
+struct gol_ctx {
+    gol_config cfg{};
+    int device = 0;
+    int nw = 0, pitch = 0, buf_rows = 0;
+    bool fast = false;
+    int band = 8;
+    uint64_t *board[2] = {nullptr, nullptr};
+    int cur = 0;
+    uint64_t *blocked = nullptr;
+    bool blocked_pending = false;
+    long long nonbinary = 0;
+    std::vector<uint8_t> raw_turn0;          // loaded bytes, kept only while non-binary & turn == 0
+    unsigned long long *counts = nullptr;    // (kRing + 1) * kShards
+    unsigned long long *h_counts = nullptr;  // pinned mirror of one slot
+    uint8_t *staging = nullptr;
+    size_t staging_size = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    long long turn = 0;
+    int halo_valid = 0;
+    std::string err;
+    std::recursive_mutex mu;
+};
+
+namespace {
+
+int fail(gol_ctx *c, int code, const char *fmt, ...)
+{
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIP_OR_FAIL(c, expr)                                                                   \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail((c), e_ == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                     \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int now = -1;
+        if (prev >= 0 && hipGetDevice(&now) == hipSuccess && now != prev) (void)hipSetDevice(prev);
+    }
+};
+
+bool is_strip(const gol_ctx *c) { return c->cfg.halo > 0; }
+
+// rows of the owned region inside the buffer
+int own_lo(const gol_ctx *c) { return c->cfg.halo; }
+int own_hi(const gol_ctx *c) { return c->cfg.halo + c->cfg.rows; }
+
+int ensure_staging(gol_ctx *c, size_t bytes)
+{
+    if (c->staging_size >= bytes) return GOL_OK;
+    if (c->staging) (void)hipFree(c->staging);
+    c->staging = nullptr;
+    c->staging_size = 0;
+    HIP_OR_FAIL(c, hipMalloc(&c->staging, bytes));
+    c->staging_size = bytes;
+    return GOL_OK;
+}
+
+void release_blocked(gol_ctx *c)
+{
+    if (c->blocked) (void)hipFree(c->blocked);
+    c->blocked = nullptr;
+    c->blocked_pending = false;
+}
+
+// popcount of owned rows of the current board -> *alive (synchronous)
+int count_now(gol_ctx *c, long long *alive)
+{
+    unsigned long long *slot = c->counts + (size_t)kRing * kShards;
+    HIP_OR_FAIL(c, hipMemsetAsync(slot, 0, kShards * sizeof(unsigned long long), c->stream));
+    HIP_OR_FAIL(c, golk::launch_popcount(c->board[c->cur], c->nw, c->pitch, own_lo(c), own_hi(c),
+                                         slot, c->stream));
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->h_counts, slot, kShards * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    unsigned long long s = 0;
+    for (int i = 0; i < kShards; i++) s += c->h_counts[i];
+    *alive = (long long)s;
+    return GOL_OK;
+}
+
+}  // namespace
+
+// ================================================================ C ABI
+extern "C" {
+
+const char *gol_strerror(int code)
+{
+    switch (code) {
+    case GOL_OK: return "ok";
+    case GOL_EINVAL: return "invalid argument";
+    case GOL_EHIP: return "HIP runtime error";
+    case GOL_ENOMEM: return "out of memory";
+    case GOL_ESTATE: return "invalid state";
+    case GOL_ENODEV: return "no HIP device";
+    case GOL_EIO: return "I/O error";
+    case GOL_ECLOSED: return "channel closed";
+    case GOL_ETIMEDOUT: return "timed out";
+    default: return "unknown error";
+    }
+}
+
+const char *gol_last_error(const gol_ctx *ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int gol_create(int32_t width, int32_t height, uint32_t flags, gol_ctx **out)
+{
+    gol_config cfg{};
+    cfg.width = width;
+    cfg.height = height;
+    cfg.device = -1;
+    cfg.row_offset = 0;
+    cfg.rows = height;
+    cfg.halo = 0;
+    cfg.flags = flags;
+    cfg.band_rows = 0;
+    return gol_create_ex(&cfg, out);
+}
+
+int gol_create_ex(const gol_config *cfg, gol_ctx **out)
+{
+    if (!cfg || !out) return GOL_EINVAL;
+    *out = nullptr;
+    if (cfg->width < 2 || cfg->height < 1 || cfg->rows < 1 || cfg->halo < 0) return GOL_EINVAL;
+    if (cfg->halo == 0 && (cfg->rows != cfg->height || cfg->row_offset != 0)) return GOL_EINVAL;
+    if (cfg->halo > 0 && (cfg->halo > cfg->rows || cfg->row_offset < 0 ||
+                          cfg->row_offset + cfg->rows > cfg->height))
+        return GOL_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return GOL_ENODEV;
+    int dev = cfg->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return GOL_ENODEV;
+    if (dev >= ndev) return GOL_ENODEV;
+
+    gol_ctx *c = new (std::nothrow) gol_ctx();
+    if (!c) return GOL_ENOMEM;
+    c->cfg = *cfg;
+    c->cfg.device = dev;
+    c->device = dev;
+    c->nw = (cfg->width + 63) / 64;
+    c->pitch = c->nw;
+    c->buf_rows = cfg->rows + 2 * cfg->halo;
+    c->fast = golk::fast_path_ok(cfg->width) && !(cfg->flags & GOL_FLAG_FORCE_GENERIC);
+    c->band = cfg->band_rows > 0 ? cfg->band_rows : golk::auto_band(cfg->width, cfg->rows);
+    c->halo_valid = cfg->halo;
+
+    DeviceGuard g(dev);
+    const size_t words = (size_t)c->buf_rows * c->pitch;
+    int rc = GOL_OK;
+    auto bail = [&](int code) {
+        gol_destroy(c);
+        return code;
+    };
+    hipError_t e;
+    if ((e = hipMalloc(&c->board[0], words * 8)) != hipSuccess ||
+        (e = hipMalloc(&c->board[1], words * 8)) != hipSuccess ||
+        (e = hipMalloc(&c->counts, (size_t)(kRing + 1) * kShards * 8)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_counts, kShards * 8, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess) {
+        rc = e == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP;
+        return bail(rc);
+    }
+    c->stream = c->own_stream;
+    if ((e = hipMemsetAsync(c->board[0], 0, words * 8, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->board[1], 0, words * 8, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->counts, 0, (size_t)(kRing + 1) * kShards * 8, c->stream)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return bail(GOL_EHIP);
+    *out = c;
+    return GOL_OK;
+}
+
+void gol_destroy(gol_ctx *c)
+{
+    if (!c) return;
+    {
+        DeviceGuard g(c->device);
+        if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+        if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+        if (c->board[0]) (void)hipFree(c->board[0]);
+        if (c->board[1]) (void)hipFree(c->board[1]);
+        if (c->blocked) (void)hipFree(c->blocked);
+        if (c->counts) (void)hipFree(c->counts);
+        if (c->staging) (void)hipFree(c->staging);
+        if (c->h_counts) (void)hipHostFree(c->h_counts);
+        if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    }
+    delete c;
+}
+
+int gol_get_info(gol_ctx *c, gol_info *info)
+{
+    if (!c || !info) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    info->width = c->cfg.width;
+    info->height = c->cfg.height;
+    info->row_offset = c->cfg.row_offset;
+    info->rows = c->cfg.rows;
+    info->halo = c->cfg.halo;
+    info->words_per_row = c->nw;
+    info->pitch_words = c->pitch;
+    info->buffer_rows = c->buf_rows;
+    info->fast_path = c->fast ? 1 : 0;
+    info->band_rows = c->band;
+    info->halo_valid = c->halo_valid;
+    info->device = c->device;
+    info->turn = c->turn;
+    info->nonbinary_cells = c->nonbinary;
+    return GOL_OK;
+}
+
+int gol_set_stream(gol_ctx *c, void *s)
+{
+    if (!c) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    // order the switch: everything queued on the old stream completes first
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return GOL_OK;
+}
+
+void *gol_get_stream(gol_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int gol_sync(gol_ctx *c)
+{
+    if (!c) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    return GOL_OK;
+}
+
+int gol_load(gol_ctx *c, const uint8_t *bytes)
+{
+    if (!c || !bytes) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const int W = c->cfg.width;
+    const size_t row_bytes = (size_t)W;
+    int chunk_rows = (int)std::max<size_t>(1, std::min<size_t>(kStagingBytes / row_bytes,
+                                                               (size_t)c->buf_rows));
+    int rc = ensure_staging(c, (size_t)chunk_rows * row_bytes);
+    if (rc) return rc;
+    release_blocked(c);
+    const size_t words = (size_t)c->buf_rows * c->pitch;
+    HIP_OR_FAIL(c, hipMalloc(&c->blocked, words * 8));
+    unsigned long long *nb = c->counts + (size_t)kRing * kShards;
+    HIP_OR_FAIL(c, hipMemsetAsync(nb, 0, kShards * 8, c->stream));
+    uint64_t *dst = c->board[0];
+    for (int r0 = 0; r0 < c->buf_rows; r0 += chunk_rows) {
+        const int nr = std::min(chunk_rows, c->buf_rows - r0);
+        HIP_OR_FAIL(c, hipMemcpyAsync(c->staging, bytes + (size_t)r0 * row_bytes,
+                                      (size_t)nr * row_bytes, hipMemcpyHostToDevice, c->stream));
+        HIP_OR_FAIL(c, golk::launch_pack(c->staging, W, nr, dst, c->blocked, c->nw, c->pitch, r0,
+                                         nb, c->stream));
+    }
+    HIP_OR_FAIL(c, hipMemcpyAsync(c->h_counts, nb, kShards * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    unsigned long long s = 0;
+    for (int i = 0; i < kShards; i++) s += c->h_counts[i];
+    c->nonbinary = (long long)s;
+    c->cur = 0;
+    c->turn = 0;
+    c->halo_valid = c->cfg.halo;
+    c->raw_turn0.clear();
+    if (s == 0) {
+        release_blocked(c);
+    } else {
+        c->blocked_pending = true;
+        // the reference returns the raw bytes unchanged at Turns = 0 (Server loop never runs)
+        const size_t own_bytes = (size_t)c->cfg.rows * row_bytes;
+        c->raw_turn0.assign(bytes + (size_t)own_lo(c) * row_bytes,
+                            bytes + (size_t)own_lo(c) * row_bytes + own_bytes);
+    }
+    return GOL_OK;
+}
+
+int gol_load_packed(gol_ctx *c, const uint64_t *words)
+{
+    if (!c || !words) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    release_blocked(c);
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(c->board[0], (size_t)c->pitch * 8, words, (size_t)c->nw * 8,
+                                    (size_t)c->nw * 8, c->buf_rows, hipMemcpyHostToDevice,
+                                    c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    c->cur = 0;
+    c->turn = 0;
+    c->nonbinary = 0;
+    c->raw_turn0.clear();
+    c->halo_valid = c->cfg.halo;
+    return GOL_OK;
+}
+
+int gol_fill_random(gol_ctx *c, uint64_t seed)
+{
+    if (!c) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    release_blocked(c);
+    const long long grow0 = (long long)c->cfg.row_offset - c->cfg.halo;
+    HIP_OR_FAIL(c, golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch,
+                                            c->buf_rows, grow0, c->cfg.height, seed, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    c->cur = 0;
+    c->turn = 0;
+    c->nonbinary = 0;
+    c->raw_turn0.clear();
+    c->halo_valid = c->cfg.halo;
+    return GOL_OK;
+}
+
+int gol_step(gol_ctx *c, int64_t turns)
+{
+    if (!c || turns < 0) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (is_strip(c) && turns > c->halo_valid)
+        return fail(c, GOL_ESTATE, "strip engine: %lld turns requested, halos valid for %d",
+                    (long long)turns, c->halo_valid);
+    DeviceGuard g(c->device);
+    const bool cnt = (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) != 0;
+    golk::StepArgs a{};
+    a.width = c->cfg.width;
+    a.nw = c->nw;
+    a.pitch = c->pitch;
+    a.modrows = c->buf_rows;
+    a.cnt_lo = own_lo(c);
+    a.cnt_hi = own_hi(c);
+    a.band = c->band;
+    for (int64_t t = 0; t < turns; ++t) {
+        if (is_strip(c)) {
+            // turn s (1-based) since the last exchange computes rows [s, buf_rows - s)
+            const int s = c->cfg.halo - c->halo_valid + 1;
+            a.row_lo = s;
+            a.row_hi = c->buf_rows - s;
+        } else {
+            a.row_lo = 0;
+            a.row_hi = c->buf_rows;
+        }
+        a.in = c->board[c->cur];
+        a.out = c->board[c->cur ^ 1];
+        a.blocked = c->blocked_pending ? c->blocked : nullptr;
+        a.counts = nullptr;
+        if (cnt) {
+            const long long next_turn = c->turn + 1;
+            const size_t slot = (size_t)(next_turn % kRing);
+            if (t % kRing == 0) {
+                // zero the slots of the next min(turns - t, kRing) turns (ring may wrap once)
+                const size_t nslots = (size_t)std::min<int64_t>(turns - t, kRing);
+                const size_t first = std::min(nslots, (size_t)kRing - slot);
+                HIP_OR_FAIL(c, hipMemsetAsync(c->counts + slot * kShards, 0,
+                                              first * kShards * 8, c->stream));
+                if (nslots > first)
+                    HIP_OR_FAIL(c, hipMemsetAsync(c->counts, 0, (nslots - first) * kShards * 8,
+                                                  c->stream));
+            }
+            a.counts = c->counts + slot * kShards;
+        }
+        HIP_OR_FAIL(c, golk::launch_step(a, c->fast, c->stream));
+        c->cur ^= 1;
+        c->turn += 1;
+        if (is_strip(c)) c->halo_valid -= 1;
+        if (c->blocked_pending) {
+            // every cell is 0/255 after the first turn; the mask is dead from here on
+            c->blocked_pending = false;
+            c->raw_turn0.clear();
+        }
+    }
+    if (c->blocked && !c->blocked_pending) {
+        HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+        release_blocked(c);
+    }
+    return GOL_OK;
+}
+
+int gol_snapshot(gol_ctx *c, int64_t *turn, int64_t *alive)
+{
+    if (!c || !turn || !alive) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    long long n = 0;
+    int rc = count_now(c, &n);
+    if (rc) return rc;
+    *turn = c->turn;
+    *alive = n;
+    return GOL_OK;
+}
+
+int gol_turn_counts(gol_ctx *c, int64_t first_turn, int64_t n, int64_t *out)
+{
+    if (!c || !out || n < 0) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!(c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN))
+        return fail(c, GOL_ESTATE, "engine created without GOL_FLAG_COUNT_EVERY_TURN");
+    if (n == 0) return GOL_OK;
+    if (first_turn < 1 || first_turn + n - 1 > c->turn || first_turn <= c->turn - kRing)
+        return fail(c, GOL_EINVAL, "turns %lld..%lld not in the recorded window",
+                    (long long)first_turn, (long long)(first_turn + n - 1));
+    DeviceGuard g(c->device);
+    std::vector<unsigned long long> h((size_t)kRing * kShards);
+    HIP_OR_FAIL(c, hipMemcpyAsync(h.data(), c->counts, h.size() * 8, hipMemcpyDeviceToHost,
+                                  c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    for (int64_t i = 0; i < n; ++i) {
+        const size_t slot = (size_t)((first_turn + i) % kRing);
+        unsigned long long s = 0;
+        for (int k = 0; k < kShards; k++) s += h[slot * kShards + k];
+        out[i] = (int64_t)s;
+    }
+    return GOL_OK;
+}
+
+int gol_read_board(gol_ctx *c, uint8_t *out)
+{
+    if (!c || !out) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    const size_t row_bytes = (size_t)c->cfg.width;
+    if (!c->raw_turn0.empty()) {
+        std::memcpy(out, c->raw_turn0.data(), c->raw_turn0.size());
+        return GOL_OK;
+    }
+    DeviceGuard g(c->device);
+    const int chunk_rows = (int)std::max<size_t>(
+        1, std::min<size_t>(kStagingBytes / row_bytes, (size_t)c->cfg.rows));
+    int rc = ensure_staging(c, (size_t)chunk_rows * row_bytes);
+    if (rc) return rc;
+    for (int r0 = 0; r0 < c->cfg.rows; r0 += chunk_rows) {
+        const int nr = std::min(chunk_rows, c->cfg.rows - r0);
+        HIP_OR_FAIL(c, golk::launch_unpack(c->board[c->cur], c->cfg.width, c->nw, c->pitch,
+                                           own_lo(c) + r0, nr, c->staging, c->stream));
+        HIP_OR_FAIL(c, hipMemcpyAsync(out + (size_t)r0 * row_bytes, c->staging,
+                                      (size_t)nr * row_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    }
+    return GOL_OK;
+}
+
+int gol_read_packed(gol_ctx *c, uint64_t *out)
+{
+    if (!c || !out) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(out, (size_t)c->nw * 8,
+                                    c->board[c->cur] + (size_t)own_lo(c) * c->pitch,
+                                    (size_t)c->pitch * 8, (size_t)c->nw * 8, c->cfg.rows,
+                                    hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    return GOL_OK;
+}
+
+int gol_alive_cells(gol_ctx *c, int64_t *xy, int64_t cap, int64_t *n)
+{
+    if (!c || !n || cap < 0 || (cap > 0 && !xy)) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const int rows = c->cfg.rows;
+    std::vector<long long> rc((size_t)rows), off((size_t)rows);
+    long long *d_rc = nullptr;
+    HIP_OR_FAIL(c, hipMalloc((void **)&d_rc, (size_t)rows * 8 * 2));
+    long long *d_off = d_rc + rows;
+    int err = GOL_OK;
+    auto done = [&](int code) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(d_rc);
+        return code;
+    };
+    hipError_t e = golk::launch_row_popcount(c->board[c->cur], c->nw, c->pitch, own_lo(c), rows,
+                                             d_rc, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(rc.data(), d_rc, (size_t)rows * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return done(fail(c, GOL_EHIP, "alive count: %s", hipGetErrorString(e)));
+    long long total = 0;
+    for (int r = 0; r < rows; r++) {
+        off[(size_t)r] = total;
+        total += rc[(size_t)r];
+    }
+    *n = total;
+    if (cap == 0 || total == 0) return done(GOL_OK);
+    // scatter in row chunks so the device list stays within the staging budget
+    const long long per_cell = 16;
+    long long r0 = 0;
+    while (r0 < rows && off[(size_t)r0] < cap) {
+        // rows [r0, r1) whose cells fit in kStagingBytes
+        long long r1 = r0;
+        while (r1 < rows && (off[(size_t)r1] + rc[(size_t)r1] - off[(size_t)r0]) * per_cell <=
+                                (long long)kStagingBytes)
+            ++r1;
+        if (r1 == r0) r1 = r0 + 1;  // a single row larger than the budget
+        const long long cells = off[(size_t)r1 - 1] + rc[(size_t)r1 - 1] - off[(size_t)r0];
+        err = ensure_staging(c, (size_t)std::max<long long>(cells * per_cell, 16));
+        if (err) return done(err);
+        // offsets relative to this chunk: subtract off[r0] via a shifted copy
+        std::vector<long long> rel((size_t)(r1 - r0));
+        for (long long r = r0; r < r1; r++) rel[(size_t)(r - r0)] = off[(size_t)r] - off[(size_t)r0];
+        e = hipMemcpyAsync(d_off + r0, rel.data(), rel.size() * 8, hipMemcpyHostToDevice,
+                           c->stream);
+        if (e == hipSuccess)
+            e = golk::launch_alive_scatter(c->board[c->cur], c->nw, c->pitch,
+                                           own_lo(c) + (int)r0, (int)(r1 - r0),
+                                           (long long)c->cfg.row_offset + r0, d_off + r0,
+                                           (long long *)c->staging, c->stream);
+        const long long want = std::min<long long>(cells, cap - off[(size_t)r0]);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(xy + 2 * off[(size_t)r0], c->staging, (size_t)want * per_cell,
+                               hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess)
+            return done(fail(c, GOL_EHIP, "alive scatter: %s", hipGetErrorString(e)));
+        r0 = r1;
+    }
+    return done(GOL_OK);
+}
+
+// ------------------------------------------------------------ halo exchange
+int gol_export_halo(gol_ctx *c, void *top, void *bottom, void *s)
+{
+    if (!c || !top || !bottom) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!is_strip(c)) return fail(c, GOL_ESTATE, "not a strip engine");
+    DeviceGuard g(c->device);
+    hipStream_t st = s ? (hipStream_t)s : c->stream;
+    if (st != c->stream) {
+        // make the caller's stream wait for the engine's queued turns
+        hipEvent_t ev;
+        HIP_OR_FAIL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_OR_FAIL(c, hipEventRecord(ev, c->stream));
+        HIP_OR_FAIL(c, hipStreamWaitEvent(st, ev, 0));
+        (void)hipEventDestroy(ev);
+    }
+    const int K = c->cfg.halo;
+    const size_t rowb = (size_t)c->nw * 8;
+    const uint64_t *b = c->board[c->cur];
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(top, rowb, b + (size_t)own_lo(c) * c->pitch,
+                                    (size_t)c->pitch * 8, rowb, K, hipMemcpyDeviceToDevice, st));
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(bottom, rowb, b + (size_t)(own_hi(c) - K) * c->pitch,
+                                    (size_t)c->pitch * 8, rowb, K, hipMemcpyDeviceToDevice, st));
+    return GOL_OK;
+}
+
+int gol_import_halo(gol_ctx *c, const void *top, const void *bottom, void *s)
+{
+    if (!c || !top || !bottom) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!is_strip(c)) return fail(c, GOL_ESTATE, "not a strip engine");
+    DeviceGuard g(c->device);
+    hipStream_t st = s ? (hipStream_t)s : c->stream;
+    const int K = c->cfg.halo;
+    const size_t rowb = (size_t)c->nw * 8;
+    uint64_t *b = c->board[c->cur];
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(b, (size_t)c->pitch * 8, top, rowb, rowb, K,
+                                    hipMemcpyDeviceToDevice, st));
+    HIP_OR_FAIL(c, hipMemcpy2DAsync(b + (size_t)own_hi(c) * c->pitch, (size_t)c->pitch * 8,
+                                    bottom, rowb, rowb, K, hipMemcpyDeviceToDevice, st));
+    if (st != c->stream) {
+        hipEvent_t ev;
+        HIP_OR_FAIL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_OR_FAIL(c, hipEventRecord(ev, st));
+        HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, ev, 0));
+        (void)hipEventDestroy(ev);
+    }
+    c->halo_valid = K;
+    return GOL_OK;
+}
+
+static int copy_rows_between(gol_ctx *dst, int dst_row, gol_ctx *src, int src_row, int K)
+{
+    if (dst->nw != src->nw) return fail(dst, GOL_EINVAL, "width mismatch");
+    // dst stream waits for src's queued work; copy on dst's stream
+    hipEvent_t ev;
+    {
+        DeviceGuard g(src->device);
+        HIP_OR_FAIL(dst, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_OR_FAIL(dst, hipEventRecord(ev, src->stream));
+    }
+    DeviceGuard g(dst->device);
+    HIP_OR_FAIL(dst, hipStreamWaitEvent(dst->stream, ev, 0));
+    const size_t rowb = (size_t)dst->nw * 8;
+    uint64_t *d = dst->board[dst->cur] + (size_t)dst_row * dst->pitch;
+    const uint64_t *s = src->board[src->cur] + (size_t)src_row * src->pitch;
+    if (dst->device == src->device) {
+        HIP_OR_FAIL(dst, hipMemcpy2DAsync(d, (size_t)dst->pitch * 8, s, (size_t)src->pitch * 8,
+                                          rowb, K, hipMemcpyDeviceToDevice, dst->stream));
+    } else {
+        // rows are contiguous when pitch == nw (always true for engines created here)
+        HIP_OR_FAIL(dst, hipMemcpyPeerAsync(d, dst->device, s, src->device, rowb * K,
+                                            dst->stream));
+    }
+    // src must not overwrite these rows before the copy lands
+    hipEvent_t back;
+    HIP_OR_FAIL(dst, hipEventCreateWithFlags(&back, hipEventDisableTiming));
+    HIP_OR_FAIL(dst, hipEventRecord(back, dst->stream));
+    {
+        DeviceGuard g2(src->device);
+        HIP_OR_FAIL(dst, hipStreamWaitEvent(src->stream, back, 0));
+    }
+    (void)hipEventDestroy(back);
+    (void)hipEventDestroy(ev);
+    return GOL_OK;
+}
+
+int gol_copy_halo_from_upper(gol_ctx *dst, gol_ctx *src)
+{
+    if (!dst || !src || !is_strip(dst) || !is_strip(src) || dst->cfg.halo != src->cfg.halo)
+        return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> l1(dst->mu);
+    std::lock_guard<std::recursive_mutex> l2(src->mu);
+    const int K = dst->cfg.halo;
+    return copy_rows_between(dst, 0, src, own_hi(src) - K, K);
+}
+
+int gol_copy_halo_from_lower(gol_ctx *dst, gol_ctx *src)
+{
+    if (!dst || !src || !is_strip(dst) || !is_strip(src) || dst->cfg.halo != src->cfg.halo)
+        return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> l1(dst->mu);
+    std::lock_guard<std::recursive_mutex> l2(src->mu);
+    const int K = dst->cfg.halo;
+    return copy_rows_between(dst, own_hi(dst), src, own_lo(src), K);
+}
+
+int gol_halo_done(gol_ctx *c)
+{
+    if (!c || !is_strip(c)) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    c->halo_valid = c->cfg.halo;
+    return GOL_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------- internal (driver) access
+namespace golint {
+long long engine_turn(gol_ctx *c) { return c->turn; }
+int engine_device(gol_ctx *c) { return c->device; }
+}  // namespace golint

@@ -1,0 +1,56 @@
+// Internal launch interface of the gfx950 kernels (gol_kernels.hip).
+// Not part of the C ABI; the engine (gol_engine.cpp) is the only caller.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace golk {
+
+constexpr int kShards = 64;            // popcount accumulator shards (one 512-B line)
+constexpr int kTileWords = 128;        // fast stencil: words per wavefront tile (64 lanes x 2)
+
+// One turn over rows [row_lo, row_hi) of a buffer of `modrows` rows (row index
+// wraps mod modrows: torus engines; strip engines never reach the wrap).
+struct StepArgs {
+    const uint64_t *in;
+    uint64_t *out;
+    const uint64_t *blocked;           // non-binary mask (turn 1 only) or nullptr
+    unsigned long long *counts;        // kShards accumulators or nullptr
+    int width;                         // cells per row
+    int nw;                            // words per row
+    int pitch;                         // row stride in words
+    int modrows;
+    int row_lo, row_hi;
+    int cnt_lo, cnt_hi;                // rows whose outputs are counted
+    int band;                          // rows per wavefront (fast) / per thread (generic)
+};
+
+bool fast_path_ok(int width);
+int auto_band(int width, int rows);
+hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);
+
+// Popcount of rows [row_lo, row_hi) into kShards accumulators (caller zeroes).
+hipError_t launch_popcount(const uint64_t *w, int nw, int pitch, int row_lo, int row_hi,
+                           unsigned long long *counts, hipStream_t s);
+
+// bytes (nrows x width, row-major, device) -> words rows [row0, row0+nrows).
+// blocked (nullable) gets the non-binary mask; nonbin accumulates its popcount.
+hipError_t launch_pack(const uint8_t *bytes, int width, int nrows, uint64_t *words,
+                       uint64_t *blocked, int nw, int pitch, int row0,
+                       unsigned long long *nonbin, hipStream_t s);
+// words rows [row0, row0+nrows) -> bytes (nrows x width, 0/255)
+hipError_t launch_unpack(const uint64_t *words, int width, int nw, int pitch, int row0,
+                         int nrows, uint8_t *bytes, hipStream_t s);
+
+// Random board: buffer row b is global row (grow0 + b) mod gheight.
+hipError_t launch_fill_random(uint64_t *words, int width, int nw, int pitch, int nrows,
+                              long long grow0, int gheight, uint64_t seed, hipStream_t s);
+
+// Alive list: per-row popcounts, then a row-major scatter of {x, y} int64 pairs.
+hipError_t launch_row_popcount(const uint64_t *w, int nw, int pitch, int row0, int nrows,
+                               long long *row_counts, hipStream_t s);
+hipError_t launch_alive_scatter(const uint64_t *w, int nw, int pitch, int row0, int nrows,
+                                long long grow0, const long long *row_offsets,
+                                long long *xy, hipStream_t s);
+
+}  // namespace golk

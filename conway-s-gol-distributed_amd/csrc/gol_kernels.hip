@@ -1,0 +1,529 @@
+// gol_kernels.hip — gfx950 (MI355X) kernels of the Game of Life engine.
+//
+// Hot path: one B3/S23 toroidal turn of a bit-packed board, the MI355X
+// replacement for the reference's byte-per-cell, branchy
+//   calculateNextState     SubServer/distributor.go:119-208
+// run over row strips by   SubServerDistributor/worker  SubServer/distributor.go:48-117
+// and the Server strips     Server/gol/distributor.go:104-134,185-224.
+//
+// Board layout in HBM: row-major, 64 cells per uint64 word, LSB = lowest x
+// (cell x of row y = bit x%64 of word y*pitch + x/64), bit set <=> byte == 255.
+//
+// K1 k_step_fast (width % 128 == 0, width >= 256) — the hot kernel.
+//   One wavefront owns a tile of 128 words (64 lanes x 16 B, one coalesced
+//   1 KiB dwordx4 access per row) and a band of `band` rows.  It walks the band
+//   top to bottom with a 3-row sliding window kept in registers, so every input
+//   row is read from HBM once per wavefront (plus 2 halo rows per band).
+//   Horizontal neighbour bits come from the adjacent lanes by DPP wave_shl /
+//   wave_shr (no LDS, no barriers: wavefronts are fully independent); the two
+//   tile-edge dwords are wave-uniform loads.  Cells are bit-sliced 32 per dword:
+//   per row  W = C<<1, E = C>>1 via v_alignbit, the 3-cell row sum (s0, s1) =
+//   (xor3, majority) — v_bitop3 on gfx950 — and per output row the 9-cell total
+//   T = sum of three 2-bit row sums; next = (T == 3) | (alive & T == 4), which is
+//   B3/S23 with the centre included.  ~14 VALU ops per 32 cells: the kernel is
+//   HBM-bound at 0.25 B per cell-update (1 bit read + 1 bit written).
+// K1g k_step_generic — any width >= 2 (16x16, 64x64 fixtures), one thread per
+//   word with explicit torus wrap for a partial last word.
+// K2 k_popcount — AliveCellsCount (Server/gol/distributor.go:173-183).
+// K3 k_row_popcount + k_alive_scatter — FinalTurnComplete's row-major alive
+//   list (Local/gol/distributor.go:229-239) by stream compaction.
+// K4 k_pack / k_unpack — PGM bytes <-> bits, with the non-binary mask.
+#include "gol_kernels.h"
+
+namespace golk {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t dpp_from_lower(uint32_t old_v, uint32_t v)
+{
+    // DPP wave_shr:1 — lane i receives lane i-1; lane 0 keeps old_v.
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old_v, (int)v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_from_upper(uint32_t old_v, uint32_t v)
+{
+    // DPP wave_shl:1 — lane i receives lane i+1; lane 63 keeps old_v.
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old_v, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+template <typename T>
+__device__ __forceinline__ T maj3(T a, T b, T c) { return (a & b) | (c & (a | b)); }
+
+// next state from three 2-bit row sums (above a, current b, below c) and the
+// centre bits: T = a + b + c over the 3x3 window incl. the centre.
+template <typename T>
+__device__ __forceinline__ T life_rule(T a0, T a1, T b0, T b1, T c0, T c1, T alive)
+{
+    const T u0 = a0 ^ b0 ^ c0;          // bit 0 of T
+    const T u1 = maj3(a0, b0, c0);      // carry of the low bits (weight 2)
+    const T v0 = a1 ^ b1 ^ c1;          // weight 2
+    const T v1 = maj3(a1, b1, c1);      // weight 4
+    // H = u1 + v0 + 2 v1 ;  T = u0 + 2 H
+    const T h1 = (u1 ^ v0) & ~v1;                       // H == 1
+    const T h2 = (u1 & v0 & ~v1) | (~(u1 | v0) & v1);   // H == 2
+    return (u0 & h1) | (~u0 & alive & h2);              // T == 3  |  (alive & T == 4)
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// block-wide sum (blockDim.x == 256) into one of kShards accumulators
+__device__ __forceinline__ void block_count(unsigned long long acc, unsigned long long *counts)
+{
+    __shared__ unsigned long long part[4];
+    acc = wave_sum(acc);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) part[w] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long s = part[0] + part[1] + part[2] + part[3];
+        if (s) atomicAdd(counts + (blockIdx.x & (kShards - 1)), s);
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ------------------------------------------------------- K1: fast stencil
+struct RowSums {
+    uint32_t s0[4], s1[4];
+};
+
+// 3-cell horizontal sums of one 128-cell lane segment.  L = the dword left of
+// c.x (bit 31 used), R = the dword right of c.w (bit 0 used).
+__device__ __forceinline__ RowSums row_sums(uint4 c, uint32_t L, uint32_t R)
+{
+    const uint32_t cc[4] = {c.x, c.y, c.z, c.w};
+    uint32_t w[4], e[4];
+    w[0] = __builtin_amdgcn_alignbit(cc[0], L, 31);      // cell x-1
+    w[1] = __builtin_amdgcn_alignbit(cc[1], cc[0], 31);
+    w[2] = __builtin_amdgcn_alignbit(cc[2], cc[1], 31);
+    w[3] = __builtin_amdgcn_alignbit(cc[3], cc[2], 31);
+    e[0] = __builtin_amdgcn_alignbit(cc[1], cc[0], 1);   // cell x+1
+    e[1] = __builtin_amdgcn_alignbit(cc[2], cc[1], 1);
+    e[2] = __builtin_amdgcn_alignbit(cc[3], cc[2], 1);
+    e[3] = __builtin_amdgcn_alignbit(R, cc[3], 1);
+    RowSums s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        s.s0[k] = w[k] ^ cc[k] ^ e[k];
+        s.s1[k] = maj3(w[k], cc[k], e[k]);
+    }
+    return s;
+}
+
+template <bool BLK, bool CNT>
+__global__ __launch_bounds__(256) void k_step_fast(const uint64_t *__restrict__ in,
+                                                   uint64_t *__restrict__ out,
+                                                   const uint64_t *__restrict__ blocked,
+                                                   unsigned long long *__restrict__ counts,
+                                                   StepArgs a, int ntx)
+{
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);   // wavefront id (uniform)
+    const int tx = wv % ntx;
+    const int by = wv / ntx;
+    const int y0 = a.row_lo + by * a.band;
+    if (y0 >= a.row_hi) return;                            // whole wavefront
+    const int y1 = min(y0 + a.band, a.row_hi);
+
+    const int nd = a.nw * 2;                               // dwords per row
+    const int tile0 = tx * (kTileWords * 2);
+    const int tile_end = min(tile0 + kTileWords * 2, nd);
+    const int d0 = tile0 + lane * 4;                       // this lane's first dword
+    const bool act = d0 < nd;
+    const int last_lane = ((tile_end - tile0) >> 2) - 1;
+    const int lidx = tile0 == 0 ? nd - 1 : tile0 - 1;      // torus wrap in x
+    const int ridx = tile_end == nd ? 0 : tile_end;
+
+    const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
+    uint32_t *out32 = reinterpret_cast<uint32_t *>(out);
+    const uint32_t *blk32 = reinterpret_cast<const uint32_t *>(blocked);
+    const size_t pitch32 = (size_t)a.pitch * 2;
+    const int M = a.modrows;
+    auto rowbase = [&](int r) -> size_t {
+        r = r < 0 ? r + M : (r >= M ? r - M : r);
+        return (size_t)r * pitch32;
+    };
+    auto load_row = [&](size_t base, uint4 &v, uint32_t &hl, uint32_t &hr) {
+        v = act ? *reinterpret_cast<const uint4 *>(in32 + base + d0) : make_uint4(0, 0, 0, 0);
+        hl = in32[base + lidx];
+        hr = in32[base + ridx];
+    };
+    auto sums = [&](uint4 v, uint32_t hl, uint32_t hr) -> RowSums {
+        const uint32_t L = dpp_from_lower(hl, v.w);
+        uint32_t R = dpp_from_upper(hr, v.x);
+        R = lane == last_lane ? hr : R;
+        return row_sums(v, L, R);
+    };
+
+    uint4 vp, vc, vn;
+    uint32_t lp, rp, lc, rc, ln, rn;
+    load_row(rowbase(y0 - 1), vp, lp, rp);
+    load_row(rowbase(y0), vc, lc, rc);
+    load_row(rowbase(y0 + 1), vn, ln, rn);
+    RowSums A = sums(vp, lp, rp);
+    RowSums B = sums(vc, lc, rc);
+    unsigned long long acc = 0;
+
+    for (int y = y0; y < y1; ++y) {
+        uint4 vq = make_uint4(0, 0, 0, 0);
+        uint32_t lq = 0, rq = 0;
+        if (y + 2 <= y1) load_row(rowbase(y + 2), vq, lq, rq);   // prefetch
+        const RowSums C = sums(vn, ln, rn);
+        const uint32_t al[4] = {vc.x, vc.y, vc.z, vc.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = life_rule(A.s0[k], A.s1[k], B.s0[k], B.s1[k], C.s0[k], C.s1[k], al[k]);
+        const size_t ob = rowbase(y);
+        if (BLK) {
+            const uint4 m = act ? *reinterpret_cast<const uint4 *>(blk32 + ob + d0)
+                                : make_uint4(0, 0, 0, 0);
+            o[0] &= ~m.x; o[1] &= ~m.y; o[2] &= ~m.z; o[3] &= ~m.w;
+        }
+        if (act) *reinterpret_cast<uint4 *>(out32 + ob + d0) = make_uint4(o[0], o[1], o[2], o[3]);
+        if (CNT && act && y >= a.cnt_lo && y < a.cnt_hi)
+            acc += __builtin_popcount(o[0]) + __builtin_popcount(o[1]) +
+                   __builtin_popcount(o[2]) + __builtin_popcount(o[3]);
+        A = B; B = C; vc = vn;
+        vn = vq; ln = lq; rn = rq;
+    }
+    if (CNT) {
+        acc = wave_sum(acc);
+        if (lane == 0 && acc) atomicAdd(counts + (wv & (kShards - 1)), acc);
+    }
+}
+
+// ---------------------------------------------------- K1g: generic stencil
+__device__ __forceinline__ uint64_t west_word(const uint64_t *row, int j, int nw, int nb)
+{
+    const uint64_t carry = j > 0 ? (row[j - 1] >> 63) : ((row[nw - 1] >> (nb - 1)) & 1ull);
+    return (row[j] << 1) | carry;
+}
+__device__ __forceinline__ uint64_t east_word(const uint64_t *row, int j, int nw, int nb)
+{
+    if (j < nw - 1) return (row[j] >> 1) | (row[j + 1] << 63);
+    return (row[j] >> 1) | ((row[0] & 1ull) << (nb - 1));
+}
+
+template <bool BLK, bool CNT>
+__global__ __launch_bounds__(256) void k_step_generic(const uint64_t *__restrict__ in,
+                                                      uint64_t *__restrict__ out,
+                                                      const uint64_t *__restrict__ blocked,
+                                                      unsigned long long *__restrict__ counts,
+                                                      StepArgs a)
+{
+    const int nb = a.width - 64 * (a.nw - 1);
+    const uint64_t lm = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+    const long long total = (long long)(a.row_hi - a.row_lo) * a.nw;
+    unsigned long long acc = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int y = a.row_lo + (int)(i / a.nw);
+        const int j = (int)(i % a.nw);
+        const int yn = y == 0 ? a.modrows - 1 : y - 1;
+        const int ys = y == a.modrows - 1 ? 0 : y + 1;
+        const uint64_t *rn = in + (size_t)yn * a.pitch;
+        const uint64_t *rc = in + (size_t)y * a.pitch;
+        const uint64_t *rs = in + (size_t)ys * a.pitch;
+        uint64_t s0[3], s1[3];
+        const uint64_t *rr[3] = {rn, rc, rs};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint64_t w = west_word(rr[k], j, a.nw, nb), c = rr[k][j],
+                           e = east_word(rr[k], j, a.nw, nb);
+            s0[k] = w ^ c ^ e;
+            s1[k] = maj3(w, c, e);
+        }
+        uint64_t o = life_rule(s0[0], s1[0], s0[1], s1[1], s0[2], s1[2], rc[j]);
+        if (j == a.nw - 1) o &= lm;
+        if (BLK) o &= ~blocked[(size_t)y * a.pitch + j];
+        out[(size_t)y * a.pitch + j] = o;
+        if (CNT && y >= a.cnt_lo && y < a.cnt_hi) acc += __builtin_popcountll(o);
+    }
+    if (CNT) block_count(acc, counts);
+}
+
+// ------------------------------------------------------------ K2: popcount
+__global__ __launch_bounds__(256) void k_popcount(const uint64_t *__restrict__ w, int nw,
+                                                  int pitch, int row_lo, int row_hi,
+                                                  unsigned long long *__restrict__ counts)
+{
+    const long long total = (long long)(row_hi - row_lo) * nw;
+    unsigned long long acc = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int y = row_lo + (int)(i / nw), j = (int)(i % nw);
+        acc += __builtin_popcountll(w[(size_t)y * pitch + j]);
+    }
+    block_count(acc, counts);
+}
+
+// ------------------------------------------------------- K4: pack / unpack
+__global__ __launch_bounds__(256) void k_pack(const uint8_t *__restrict__ bytes, int width,
+                                              int nrows, uint64_t *__restrict__ words,
+                                              uint64_t *__restrict__ blocked, int nw, int pitch,
+                                              int row0, unsigned long long *__restrict__ nonbin)
+{
+    const long long total = (long long)nrows * nw;
+    unsigned long long acc = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int y = (int)(i / nw), j = (int)(i % nw);
+        const uint8_t *src = bytes + (size_t)y * width + (size_t)64 * j;
+        const int n = min(64, width - 64 * j);
+        uint64_t al = 0, bl = 0;
+        if (n == 64 && (width & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = reinterpret_cast<const uint4 *>(src)[q];
+                const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const uint32_t b = (d[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                    al |= (uint64_t)(b == 255u) << (16 * q + k);
+                    bl |= (uint64_t)(b != 255u && b != 0u) << (16 * q + k);
+                }
+            }
+        } else {
+            for (int k = 0; k < n; ++k) {
+                const uint32_t b = src[k];
+                al |= (uint64_t)(b == 255u) << k;
+                bl |= (uint64_t)(b != 255u && b != 0u) << k;
+            }
+        }
+        words[(size_t)(row0 + y) * pitch + j] = al;
+        if (blocked) blocked[(size_t)(row0 + y) * pitch + j] = bl;
+        acc += __builtin_popcountll(bl);
+    }
+    block_count(acc, nonbin);
+}
+
+__global__ __launch_bounds__(256) void k_unpack(const uint64_t *__restrict__ words, int width,
+                                                int nw, int pitch, int row0, int nrows,
+                                                uint8_t *__restrict__ bytes)
+{
+    const long long total = (long long)nrows * nw;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int y = (int)(i / nw), j = (int)(i % nw);
+        const uint64_t w = words[(size_t)(row0 + y) * pitch + j];
+        uint8_t *dst = bytes + (size_t)y * width + (size_t)64 * j;
+        const int n = min(64, width - 64 * j);
+        if (n == 64 && (width & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t d[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const uint32_t bits = (uint32_t)(w >> (16 * q + 4 * m)) & 0xfu;
+                    d[m] = ((bits & 1u) ? 0xffu : 0u) | ((bits & 2u) ? 0xff00u : 0u) |
+                           ((bits & 4u) ? 0xff0000u : 0u) | ((bits & 8u) ? 0xff000000u : 0u);
+                }
+                reinterpret_cast<uint4 *>(dst)[q] = make_uint4(d[0], d[1], d[2], d[3]);
+            }
+        } else {
+            for (int k = 0; k < n; ++k) dst[k] = ((w >> k) & 1ull) ? 255 : 0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fill_random(uint64_t *__restrict__ words, int width,
+                                                     int nw, int pitch, int nrows,
+                                                     long long grow0, int gheight,
+                                                     uint64_t seed)
+{
+    const int nb = width - 64 * (nw - 1);
+    const uint64_t lm = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+    const long long total = (long long)nrows * nw;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int b = (int)(i / nw), j = (int)(i % nw);
+        long long g = (grow0 + b) % gheight;
+        if (g < 0) g += gheight;
+        uint64_t v = splitmix64((seed << 40) + (uint64_t)g * nw + j);
+        if (j == nw - 1) v &= lm;
+        words[(size_t)b * pitch + j] = v;
+    }
+}
+
+// ------------------------------------------------------- K3: alive list
+// One wavefront per row.
+__global__ __launch_bounds__(256) void k_row_popcount(const uint64_t *__restrict__ w, int nw,
+                                                      int pitch, int row0, int nrows,
+                                                      long long *__restrict__ row_counts)
+{
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nrows) return;
+    const uint64_t *row = w + (size_t)(row0 + r) * pitch;
+    unsigned long long acc = 0;
+    for (int j = lane; j < nw; j += 64) acc += __builtin_popcountll(row[j]);
+    acc = wave_sum(acc);
+    if (lane == 0) row_counts[r] = (long long)acc;
+}
+
+__global__ __launch_bounds__(256) void k_alive_scatter(const uint64_t *__restrict__ w, int nw,
+                                                       int pitch, int row0, int nrows,
+                                                       long long grow0,
+                                                       const long long *__restrict__ row_off,
+                                                       long long *__restrict__ xy)
+{
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nrows) return;
+    const uint64_t *row = w + (size_t)(row0 + r) * pitch;
+    long long base = row_off[r];
+    const long long y = grow0 + r;
+    for (int j0 = 0; j0 < nw; j0 += 64) {
+        const int j = j0 + lane;
+        uint64_t v = j < nw ? row[j] : 0ull;
+        const int c = __builtin_popcountll(v);
+        // inclusive scan of c across the wavefront
+        int incl = c;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += t;
+        }
+        long long o = base + incl - c;
+        while (v) {
+            const int b = __builtin_ctzll(v);
+            xy[2 * o] = 64LL * j + b;
+            xy[2 * o + 1] = y;
+            ++o;
+            v &= v - 1;
+        }
+        base += __shfl(incl, 63, 64);
+    }
+}
+
+// ------------------------------------------------------------- launchers
+static inline int grid_for(long long total, int cap = 2048)
+{
+    long long g = (total + 255) / 256;
+    if (g < 1) g = 1;
+    return (int)(g > cap ? cap : g);
+}
+
+bool fast_path_ok(int width) { return width >= 256 && (width % 128) == 0; }
+
+int auto_band(int width, int rows)
+{
+    const int nw = (width + 63) / 64;
+    const long long ntx = fast_path_ok(width) ? (nw + kTileWords - 1) / kTileWords : 1;
+    const long long row_tiles = (long long)rows * ntx;
+    // aim for ~8192 wavefronts (32 per CU on 256 CUs); keep bands >= 8 rows so
+    // the 2 halo rows per band stay a small re-read, <= 128 to bound the tail.
+    long long b = row_tiles / 8192;
+    if (b < 8) b = 8;
+    if (b > 128) b = 128;
+    return (int)b;
+}
+
+hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
+{
+    if (a.row_hi <= a.row_lo) return hipSuccess;
+    const bool blk = a.blocked != nullptr, cnt = a.counts != nullptr;
+    if (fast) {
+        const int ntx = (a.nw + kTileWords - 1) / kTileWords;
+        const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
+        const long long nwaves = (long long)ntx * nbands;
+        const int blocks = (int)((nwaves + 3) / 4);
+        if (blk && cnt)
+            hipLaunchKernelGGL((k_step_fast<true, true>), dim3(blocks), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a, ntx);
+        else if (blk)
+            hipLaunchKernelGGL((k_step_fast<true, false>), dim3(blocks), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a, ntx);
+        else if (cnt)
+            hipLaunchKernelGGL((k_step_fast<false, true>), dim3(blocks), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a, ntx);
+        else
+            hipLaunchKernelGGL((k_step_fast<false, false>), dim3(blocks), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a, ntx);
+    } else {
+        const int g = grid_for((long long)(a.row_hi - a.row_lo) * a.nw);
+        if (blk && cnt)
+            hipLaunchKernelGGL((k_step_generic<true, true>), dim3(g), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a);
+        else if (blk)
+            hipLaunchKernelGGL((k_step_generic<true, false>), dim3(g), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a);
+        else if (cnt)
+            hipLaunchKernelGGL((k_step_generic<false, true>), dim3(g), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a);
+        else
+            hipLaunchKernelGGL((k_step_generic<false, false>), dim3(g), dim3(256), 0, s, a.in,
+                               a.out, a.blocked, a.counts, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_popcount(const uint64_t *w, int nw, int pitch, int row_lo, int row_hi,
+                           unsigned long long *counts, hipStream_t s)
+{
+    const int g = grid_for((long long)(row_hi - row_lo) * nw, 1024);
+    hipLaunchKernelGGL(k_popcount, dim3(g), dim3(256), 0, s, w, nw, pitch, row_lo, row_hi,
+                       counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const uint8_t *bytes, int width, int nrows, uint64_t *words,
+                       uint64_t *blocked, int nw, int pitch, int row0,
+                       unsigned long long *nonbin, hipStream_t s)
+{
+    const int g = grid_for((long long)nrows * nw);
+    hipLaunchKernelGGL(k_pack, dim3(g), dim3(256), 0, s, bytes, width, nrows, words, blocked,
+                       nw, pitch, row0, nonbin);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const uint64_t *words, int width, int nw, int pitch, int row0,
+                         int nrows, uint8_t *bytes, hipStream_t s)
+{
+    const int g = grid_for((long long)nrows * nw);
+    hipLaunchKernelGGL(k_unpack, dim3(g), dim3(256), 0, s, words, width, nw, pitch, row0, nrows,
+                       bytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_random(uint64_t *words, int width, int nw, int pitch, int nrows,
+                              long long grow0, int gheight, uint64_t seed, hipStream_t s)
+{
+    const int g = grid_for((long long)nrows * nw);
+    hipLaunchKernelGGL(k_fill_random, dim3(g), dim3(256), 0, s, words, width, nw, pitch, nrows,
+                       grow0, gheight, seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_popcount(const uint64_t *w, int nw, int pitch, int row0, int nrows,
+                               long long *row_counts, hipStream_t s)
+{
+    const int blocks = (nrows + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_row_popcount, dim3(blocks), dim3(256), 0, s, w, nw, pitch, row0, nrows,
+                       row_counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_alive_scatter(const uint64_t *w, int nw, int pitch, int row0, int nrows,
+                                long long grow0, const long long *row_offsets, long long *xy,
+                                hipStream_t s)
+{
+    const int blocks = (nrows + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_alive_scatter, dim3(blocks), dim3(256), 0, s, w, nw, pitch, row0,
+                       nrows, grow0, row_offsets, xy);
+    return hipGetLastError();
+}
+
+}  // namespace golk

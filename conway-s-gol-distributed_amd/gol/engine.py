@@ -1,0 +1,180 @@
+"""Engine: a Python handle on one gol_ctx (include/gol_amd.h).
+
+One Engine = one MI355X holding the whole torus board or one row strip of it —
+the GPU-resident replacement for the reference's SubServer
+(``API.SubServerDistributor``, reference ``SubServer/distributor.go:48-84``)
+plus the Server's per-turn commit and counters
+(``Server/gol/distributor.go:62-75,104-134,173-183``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+
+class Engine:
+    def __init__(self, width: int, height: int, *, device: int = -1, row_offset: int = 0,
+                 rows: int | None = None, halo: int = 0, count_every_turn: bool = False,
+                 force_generic: bool = False, band_rows: int = 0):
+        L = N.lib()
+        cfg = N.gol_config()
+        cfg.width, cfg.height = int(width), int(height)
+        cfg.device = int(device)
+        cfg.row_offset = int(row_offset)
+        cfg.rows = int(height if rows is None else rows)
+        cfg.halo = int(halo)
+        cfg.flags = ((N.GOL_FLAG_COUNT_EVERY_TURN if count_every_turn else 0) |
+                     (N.GOL_FLAG_FORCE_GENERIC if force_generic else 0))
+        cfg.band_rows = int(band_rows)
+        h = ctypes.c_void_p()
+        N.check(L.gol_create_ex(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self._L = L
+        info = self.info()
+        self.width, self.height = info.width, info.height
+        self.rows, self.halo = info.rows, info.halo
+        self.row_offset = info.row_offset
+        self.words_per_row = info.words_per_row
+        self.buffer_rows = info.buffer_rows
+
+    # -- lifetime
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.gol_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _c(self, rc):
+        return N.check(rc, self._h)
+
+    # -- info / streams
+    def info(self) -> N.gol_info:
+        i = N.gol_info()
+        self._c(self._L.gol_get_info(self._h, ctypes.byref(i)))
+        return i
+
+    @property
+    def turn(self) -> int:
+        return int(self.info().turn)
+
+    @property
+    def halo_valid(self) -> int:
+        return int(self.info().halo_valid)
+
+    def set_stream(self, stream_ptr: int | None):
+        self._c(self._L.gol_set_stream(self._h, ctypes.c_void_p(stream_ptr or 0)))
+
+    def stream(self) -> int:
+        return int(self._L.gol_get_stream(self._h) or 0)
+
+    def sync(self):
+        self._c(self._L.gol_sync(self._h))
+
+    # -- boards
+    def load(self, board: np.ndarray):
+        """bytes (buffer_rows, width): whole board, or the haloed strip."""
+        b = np.ascontiguousarray(board, dtype=np.uint8)
+        if b.shape != (self.buffer_rows, self.width):
+            raise ValueError(f"expected {(self.buffer_rows, self.width)}, got {b.shape}")
+        self._c(self._L.gol_load(self._h, b.ctypes.data_as(N._u8p)))
+
+    def load_packed(self, words: np.ndarray):
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        if w.shape != (self.buffer_rows, self.words_per_row):
+            raise ValueError(f"expected {(self.buffer_rows, self.words_per_row)}, got {w.shape}")
+        self._c(self._L.gol_load_packed(self._h, w.ctypes.data_as(N._u64p)))
+
+    def fill_random(self, seed: int):
+        self._c(self._L.gol_fill_random(self._h, ctypes.c_uint64(int(seed))))
+
+    def step(self, turns: int = 1):
+        self._c(self._L.gol_step(self._h, int(turns)))
+
+    def snapshot(self):
+        """(completed turns, alive cells) — the reference's Alivecount pair."""
+        t, a = ctypes.c_int64(), ctypes.c_int64()
+        self._c(self._L.gol_snapshot(self._h, ctypes.byref(t), ctypes.byref(a)))
+        return int(t.value), int(a.value)
+
+    def turn_counts(self, first_turn: int, n: int) -> np.ndarray:
+        out = np.zeros(max(int(n), 1), dtype=np.int64)
+        self._c(self._L.gol_turn_counts(self._h, int(first_turn), int(n),
+                                        out.ctypes.data_as(N._i64p)))
+        return out[: int(n)]
+
+    def read_board(self) -> np.ndarray:
+        out = np.zeros((self.rows, self.width), dtype=np.uint8)
+        self._c(self._L.gol_read_board(self._h, out.ctypes.data_as(N._u8p)))
+        return out
+
+    def read_packed(self) -> np.ndarray:
+        out = np.zeros((self.rows, self.words_per_row), dtype=np.uint64)
+        self._c(self._L.gol_read_packed(self._h, out.ctypes.data_as(N._u64p)))
+        return out
+
+    def alive_cells(self) -> np.ndarray:
+        """Row-major (n, 2) int64 {x, y} list (Local/gol/distributor.go:229-239)."""
+        n = ctypes.c_int64()
+        self._c(self._L.gol_alive_cells(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros((max(n.value, 1), 2), dtype=np.int64)
+        if n.value:
+            self._c(self._L.gol_alive_cells(self._h, out.ctypes.data_as(N._i64p), n.value,
+                                            ctypes.byref(n)))
+        return out[: n.value]
+
+    # -- strip halo exchange (device pointers)
+    def export_halo(self, top_ptr: int, bottom_ptr: int, stream_ptr: int | None = None):
+        self._c(self._L.gol_export_halo(self._h, ctypes.c_void_p(top_ptr),
+                                        ctypes.c_void_p(bottom_ptr),
+                                        ctypes.c_void_p(stream_ptr or 0)))
+
+    def import_halo(self, top_ptr: int, bottom_ptr: int, stream_ptr: int | None = None):
+        self._c(self._L.gol_import_halo(self._h, ctypes.c_void_p(top_ptr),
+                                        ctypes.c_void_p(bottom_ptr),
+                                        ctypes.c_void_p(stream_ptr or 0)))
+
+    def copy_halo_from_upper(self, upper: "Engine"):
+        self._c(self._L.gol_copy_halo_from_upper(self._h, upper._h))
+
+    def copy_halo_from_lower(self, lower: "Engine"):
+        self._c(self._L.gol_copy_halo_from_lower(self._h, lower._h))
+
+    def halo_done(self):
+        self._c(self._L.gol_halo_done(self._h))
+
+
+def strip_split(height: int, n: int):
+    """The reference Server's row split (Server/gol/distributor.go:106-116):
+    base = H // n rows each, the first H % n strips one more.  Returns [(offset, rows)]."""
+    base, slack = divmod(int(height), int(n))
+    out, off = [], 0
+    for i in range(int(n)):
+        r = base + (1 if i < slack else 0)
+        out.append((off, r))
+        off += r
+    return out
+
+
+def haloed_rows(board: np.ndarray, offset: int, rows: int, halo: int) -> np.ndarray:
+    """Global rows offset-halo .. offset+rows+halo-1 (mod H) of a byte board."""
+    H = board.shape[0]
+    idx = (np.arange(offset - halo, offset + rows + halo) % H)
+    return np.ascontiguousarray(board[idx])

@@ -1,0 +1,212 @@
+/*
+ * gol_amd.h — C ABI of the MI355X-native Game of Life engine (libgolamd.so).
+ *
+ * Drop-in boundary for the reference's per-turn board update
+ * (joyce-leesw/Conway-s-GOL-Distributed).  The reference crosses this boundary
+ * with Go net/rpc calls whose payload is a gob-encoded [][]uint8 board; here it
+ * is a plain C ABI (opaque handles, pointers + sizes, int error codes, no
+ * exceptions and no torch types), so a cgo / ctypes / JNI binding is a thin stub
+ * (INTEGRATION.md shows the cgo one).
+ *
+ * Two layers:
+ *
+ *  1. Engine (gol_ctx): one MI355X, one board or one row strip of a board.
+ *     Owns every device buffer (double-buffered bit-packed board, 64 cells per
+ *     uint64 word, LSB = lowest x; optional non-binary "blocked" mask; popcount
+ *     shards).  Replaces, per GPU:
+ *       API.SubServerDistributor          SubServer/distributor.go:48-84
+ *       calculateNextState                SubServer/distributor.go:119-208
+ *       the Server turn loop + commit     Server/gol/distributor.go:104-134
+ *       API.Alivecount / calculateAliveCells  Server/gol/distributor.go:69-75,173-183
+ *       API.GetWorld                      Server/gol/distributor.go:62-67
+ *       Local calculateAliveCells         Local/gol/distributor.go:229-239
+ *
+ *  2. Run driver (gol_run): the C++ host mirror of
+ *       gol.Run(Params, events chan<- Event, keyPresses <-chan rune)
+ *                                         Local/gol/gol.go:12-40
+ *     with the distributor's event sequence (Local/gol/distributor.go:55-227),
+ *     the 2 s AliveCellsCount ticker (:58,154-167), the s/p/q/k key handling
+ *     (:107-152, Server/gol/distributor.go:136-164) and the PGM I/O goroutine
+ *     (Local/gol/io.go:42-143).
+ *
+ * Threading: an engine is driven by one thread at a time (every call takes the
+ * engine's lock, as the reference Server's mutex serialises GetWorld/Alivecount
+ * with the commit: Server/gol/distributor.go:63-73,131-134).  A run driver owns
+ * its engines on its own thread; gol_run_* calls are thread-safe.
+ */
+#ifndef GOL_AMD_H
+#define GOL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------ error codes */
+#define GOL_OK          0
+#define GOL_EINVAL     -1   /* bad argument (size, null pointer, W < 2, ...)        */
+#define GOL_EHIP       -2   /* HIP runtime error (message in gol_last_error)         */
+#define GOL_ENOMEM     -3   /* device or host allocation failed                      */
+#define GOL_ESTATE     -4   /* call not valid now (e.g. halo exhausted in strip mode)*/
+#define GOL_ENODEV     -5   /* no usable HIP device                                  */
+#define GOL_EIO        -6   /* PGM file missing / malformed (reference: panic)       */
+#define GOL_ECLOSED    -7   /* run driver: event channel closed                      */
+#define GOL_ETIMEDOUT  -8   /* run driver: no event within the timeout               */
+
+/* ----------------------------------------------------------------- engine */
+typedef struct gol_ctx gol_ctx;
+
+/* flags */
+#define GOL_FLAG_COUNT_EVERY_TURN  0x1u  /* fuse a popcount into every turn (per-turn series) */
+#define GOL_FLAG_FORCE_GENERIC     0x2u  /* use the generic stencil even when the fast one applies */
+
+typedef struct gol_config {
+    int32_t  width;       /* Params.ImageWidth  (>= 2)                                   */
+    int32_t  height;      /* Params.ImageHeight of the WHOLE board (>= 1)                */
+    int32_t  device;      /* HIP device ordinal; -1 = current device                     */
+    int32_t  row_offset;  /* first global row owned by this engine                        */
+    int32_t  rows;        /* rows owned; rows == height and halo == 0 => torus engine      */
+    int32_t  halo;        /* strip mode: halo depth K in rows (1 <= K <= rows)            */
+    uint32_t flags;       /* GOL_FLAG_*                                                   */
+    int32_t  band_rows;   /* rows per wavefront band in the stencil; 0 = auto             */
+} gol_config;
+
+typedef struct gol_info {
+    int32_t  width, height, row_offset, rows, halo;
+    int32_t  words_per_row;     /* ceil(width / 64)                                  */
+    int32_t  pitch_words;       /* row stride of the device board in uint64 words    */
+    int32_t  buffer_rows;       /* rows + 2 * halo                                   */
+    int32_t  fast_path;         /* 1 = the LDS-free DPP stencil (width % 128 == 0, >= 256) */
+    int32_t  band_rows;         /* effective band height                              */
+    int32_t  halo_valid;        /* strip mode: turns left before the next exchange    */
+    int32_t  device;
+    int64_t  turn;              /* completed turns since load                          */
+    int64_t  nonbinary_cells;   /* cells that were neither 0 nor 255 at load           */
+} gol_info;
+
+/* Whole-board (torus) engine on the current device. */
+int  gol_create(int32_t width, int32_t height, uint32_t flags, gol_ctx **out);
+/* Whole-board or row-strip engine (see gol_config). */
+int  gol_create_ex(const gol_config *cfg, gol_ctx **out);
+void gol_destroy(gol_ctx *ctx);
+const char *gol_last_error(const gol_ctx *ctx);   /* per engine; "" if none            */
+const char *gol_strerror(int code);
+int  gol_get_info(gol_ctx *ctx, gol_info *info);
+
+/* Stream: the engine creates its own HIP stream; gol_set_stream makes it enqueue
+ * on the caller's stream instead (e.g. torch.cuda.current_stream().cuda_stream).
+ * NULL restores the engine's own stream. */
+int   gol_set_stream(gol_ctx *ctx, void *hip_stream);
+void *gol_get_stream(gol_ctx *ctx);
+int   gol_sync(gol_ctx *ctx);
+
+/* Load a board from host bytes (0 = dead, 255 = alive, anything else: the
+ * reference's non-binary semantics).  Torus engine: height x width bytes.
+ * Strip engine: (rows + 2*halo) x width bytes = global rows
+ * row_offset-halo .. row_offset+rows+halo-1 (mod height).  Resets turn to 0. */
+int gol_load(gol_ctx *ctx, const uint8_t *bytes);
+/* Synthetic board: word (y, j) = splitmix64((seed << 40) + y*words_per_row + j),
+ * y the GLOBAL row (oracle/bitref.c uses the same definition).  Resets turn. */
+int gol_fill_random(gol_ctx *ctx, uint64_t seed);
+/* Load / read packed words for the buffer rows (strip: incl. halos), row stride
+ * words_per_row, for checkers that work on packed boards. */
+int gol_load_packed(gol_ctx *ctx, const uint64_t *words);
+
+/* Advance `turns` turns.  Torus engine: any turns >= 0.  Strip engine:
+ * turns <= halo_valid (then exchange halos; see gol_export_halo). */
+int gol_step(gol_ctx *ctx, int64_t turns);
+
+/* Consistent (turn, alive) pair of the current board (owned rows only). */
+int gol_snapshot(gol_ctx *ctx, int64_t *turn, int64_t *alive);
+/* Per-turn alive counts recorded by GOL_FLAG_COUNT_EVERY_TURN for turns
+ * first_turn .. first_turn+n-1 (must be among the last 4096 turns). */
+int gol_turn_counts(gol_ctx *ctx, int64_t first_turn, int64_t n, int64_t *out);
+
+/* Owned rows as bytes (rows x width, 0/255; at turn 0 the loaded bytes as-is,
+ * matching the reference's Turns = 0 output). */
+int gol_read_board(gol_ctx *ctx, uint8_t *out);
+/* Owned rows as packed words (rows x words_per_row). */
+int gol_read_packed(gol_ctx *ctx, uint64_t *out);
+/* Row-major alive-cell list {x, y} (y = global row) of the owned rows, as
+ * int64 pairs; writes min(n, cap) pairs and sets *n to the total. */
+int gol_alive_cells(gol_ctx *ctx, int64_t *xy, int64_t cap, int64_t *n);
+
+/* Strip mode halo exchange.  export: copy the first and the last `halo` owned
+ * rows (packed, halo x words_per_row uint64 each) to device buffers `top` and
+ * `bottom` on `hip_stream` (NULL = engine stream).  import: copy the neighbour
+ * rows into this engine's halos (top = the rows above, from rank r-1's bottom;
+ * bottom = the rows below, from rank r+1's top) and reset halo_valid to halo. */
+int gol_export_halo(gol_ctx *ctx, void *top, void *bottom, void *hip_stream);
+int gol_import_halo(gol_ctx *ctx, const void *top, const void *bottom, void *hip_stream);
+/* In-process exchange between two strip engines (any devices, peer copies):
+ * dst's top halo <- src's last `halo` owned rows (src is dst's upper neighbour). */
+int gol_copy_halo_from_upper(gol_ctx *dst, gol_ctx *src);
+/* dst's bottom halo <- src's first `halo` owned rows (src is dst's lower neighbour). */
+int gol_copy_halo_from_lower(gol_ctx *dst, gol_ctx *src);
+/* Mark the halos fresh after all copies into this engine are enqueued. */
+int gol_halo_done(gol_ctx *ctx);
+
+/* -------------------------------------------------------------- run driver */
+typedef struct gol_params {          /* Local/gol/gol.go:4-9 */
+    int64_t turns;
+    int32_t threads;                 /* kept for API parity; the GPU result is independent of it */
+    int32_t image_width;
+    int32_t image_height;
+} gol_params;
+
+typedef enum gol_event_type {        /* Local/gol/event.go:9-68 */
+    GOL_EV_ALIVE_CELLS_COUNT    = 1,
+    GOL_EV_IMAGE_OUTPUT_COMPLETE = 2,
+    GOL_EV_STATE_CHANGE         = 3,
+    GOL_EV_CELL_FLIPPED         = 4,
+    GOL_EV_TURN_COMPLETE        = 5,
+    GOL_EV_FINAL_TURN_COMPLETE  = 6
+} gol_event_type;
+
+typedef enum gol_state { GOL_PAUSED = 0, GOL_EXECUTING = 1, GOL_QUITTING = 2 } gol_state;
+
+typedef struct gol_event {
+    int32_t type;                    /* gol_event_type                                  */
+    int32_t new_state;               /* StateChange.NewState                            */
+    int64_t completed_turns;         /* every event's GetCompletedTurns()               */
+    int64_t cells_count;             /* AliveCellsCount.CellsCount; FinalTurnComplete: len(Alive) */
+    int64_t x, y;                    /* CellFlipped.Cell                                */
+    char    filename[256];           /* ImageOutputComplete.Filename                    */
+} gol_event;
+
+typedef struct gol_run_options {
+    const char *image_dir;           /* where {W}x{H}.pgm is read ("images")            */
+    const char *out_dir;             /* where {W}x{H}x{T}.pgm is written ("out")        */
+    int32_t ngpus;                   /* row strips = engines (the reference's len(SUB)); 0 = 1 */
+    const int32_t *devices;          /* ngpus device ordinals, NULL = 0..ngpus-1 (mod device count) */
+    int32_t halo;                    /* strip halo depth K; 0 = auto                    */
+    int32_t ticker_ms;               /* AliveCellsCount period; 0 = 2000 (distributor.go:58) */
+    int32_t event_capacity;          /* bounded event channel; 0 = 1 (unbuffered-like)  */
+    int32_t emit_turn_complete;      /* 1 = TurnComplete{t} for every turn (event.go:55-60) */
+    int32_t emit_cell_flipped;       /* 1 = CellFlipped for initial cells and each flip  */
+    uint32_t engine_flags;           /* GOL_FLAG_* for the engines                      */
+} gol_run_options;
+
+typedef struct gol_run gol_run;
+
+/* Start a run (non-blocking, like gol.Run).  opts may be NULL (defaults). */
+int gol_run_start(const gol_params *p, const gol_run_options *opts, gol_run **out);
+/* Receive the next event: GOL_OK, GOL_ECLOSED once the channel is closed and
+ * drained, GOL_ETIMEDOUT after timeout_ms (< 0 = wait forever). */
+int gol_run_next_event(gol_run *r, gol_event *ev, int32_t timeout_ms);
+/* FinalTurnComplete.Alive of the most recently received FinalTurnComplete:
+ * writes min(n, cap) {x, y} int64 pairs, returns n (or < 0 on error). */
+int64_t gol_run_final_alive(gol_run *r, int64_t *xy, int64_t cap);
+/* keyPresses <- rune ('s', 'p', 'q', 'k'). */
+int gol_run_key(gol_run *r, int32_t rune);
+/* Error text of a run that failed (the events channel is closed early). */
+const char *gol_run_error(gol_run *r);
+/* Join the driver thread and free the run. */
+void gol_run_destroy(gol_run *r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOL_AMD_H */

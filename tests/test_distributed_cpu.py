@@ -1,0 +1,98 @@
+"""The N > 1 strip path's partition + halo exchange (gol/distributed.py) over gloo
+on CPU, world sizes 2-4.  The per-rank compute here is an oracle-backed stand-in
+(test-only) behind the same strip interface the HIP EngineStrip implements; the
+exchange code under test is the product's DistStrip, unchanged."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class OracleStrip:
+    """Test stand-in for EngineStrip: a byte strip with K halo rows, stepped by the
+    numpy oracle (rows outside the valid trapezoid are garbage, as on the GPU)."""
+
+    def __init__(self, board, offset, rows, K):
+        from gol import haloed_rows
+        self.buf = haloed_rows(board, offset, rows, K)
+        self.K, self.rows = K, rows
+        self.halo_valid = K
+        self.turns = 0
+
+    def step(self, n):
+        from oracle import oracle as O
+        assert n <= self.halo_valid
+        for _ in range(n):
+            self.buf = O.np_step(self.buf)
+        self.halo_valid -= n
+        self.turns += n
+
+    def export_rows(self):
+        K = self.K
+        top = torch.from_numpy(self.buf[K:2 * K].copy())
+        bot = torch.from_numpy(self.buf[self.rows:self.rows + K].copy())
+        return top, bot
+
+    def recv_buffers(self):
+        shape = (self.K, self.buf.shape[1])
+        return torch.empty(shape, dtype=torch.uint8), torch.empty(shape, dtype=torch.uint8)
+
+    def import_rows(self, top, bottom):
+        K = self.K
+        self.buf[:K] = top.numpy()
+        self.buf[K + self.rows:] = bottom.numpy()
+        self.halo_valid = K
+
+    def owned(self):
+        return self.buf[self.K:self.K + self.rows]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, K, turns, w, h, outdir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "conway-s-gol-distributed_amd"), root):
+        sys.path.insert(0, p)
+    from gol import strip_split
+    from gol.distributed import DistStrip
+    from oracle import oracle as O
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    board = O.unpack(O.gen_random(21, w, h), w)
+    off, rows = strip_split(h, world)[rank]
+    Kp = min(K, min(r for _, r in strip_split(h, world)))
+    strip = OracleStrip(board, off, rows, Kp)
+    ds = DistStrip(strip, rank, world)
+    ds.step(turns)
+    np.save(os.path.join(outdir, f"r{rank}.npy"), strip.owned())
+    with open(os.path.join(outdir, f"x{rank}.txt"), "w") as f:
+        f.write(str(ds.exchanges))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,K,turns", [(2, 3, 10), (2, 1, 5), (3, 4, 13), (4, 2, 9)])
+def test_gloo_strip_exchange_matches_torus(world, K, turns):
+    from oracle import oracle as O
+    w, h = 70, 37
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), K, turns, w, h, d), nprocs=world,
+                 join=True)
+        got = np.concatenate([np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)])
+        nx = [int(open(os.path.join(d, f"x{r}.txt")).read()) for r in range(world)]
+    want = O.np_run(O.unpack(O.gen_random(21, w, h), w), turns)
+    assert np.array_equal(got, want)
+    Kp = min(K, h // world)
+    assert nx == [(turns - 1) // Kp] * world

@@ -1,0 +1,272 @@
+"""Parity of the HIP engine (through the C ABI) against the reference's golden
+fixtures and the CPU oracle.  Bit-exact everywhere: this is integer/bit work.
+
+Reference behaviour being checked: calculateNextState
+(SubServer/distributor.go:119-208) under the Server/SubServer strip splits
+(Server/gol/distributor.go:104-134,185-224), the alive count
+(Server/gol/distributor.go:173-183) and the alive list
+(Local/gol/distributor.go:229-239); fixtures Local/check/images,
+Local/check/alive (tests/golden/).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import golden_data as G
+
+pytestmark = pytest.mark.gpu
+
+SIZES = (16, 64, 512)
+
+
+@pytest.fixture(scope="module")
+def gol():
+    import gol as g
+    return g
+
+
+def _engine(gol, w, h, **kw):
+    return gol.Engine(w, h, device=0, **kw)
+
+
+# --------------------------------------------------------------- fixtures
+@pytest.mark.parametrize("size", SIZES)
+@pytest.mark.parametrize("turns", (0, 1, 100))
+def test_check_images(gol, oracle, size, turns):
+    """TestGol / TestPgm matrix: Local/check/images/{size}x{size}x{turns}.pgm."""
+    exp = G.check_board(size, turns)
+    with _engine(gol, size, size) as e:
+        e.load(G.input_board(size))
+        e.step(turns)
+        got = e.read_board()
+        assert np.array_equal(got, exp)
+        t, alive = e.snapshot()
+        assert (t, alive) == (turns, int((exp == 255).sum()))
+        cells = e.alive_cells()
+        assert np.array_equal(cells, oracle.ref_alive_cells(exp))
+
+
+@pytest.mark.parametrize("size", SIZES)
+def test_alive_series_10000(gol, size):
+    """Local/check/alive/{size}x{size}.csv: every turn 1..10000 (fused popcount)."""
+    series = G.alive_series(size)
+    with _engine(gol, size, size, count_every_turn=True) as e:
+        e.load(G.input_board(size))
+        got = []
+        done = 0
+        while done < 10000:
+            n = min(4000, 10000 - done)
+            e.step(n)
+            got.extend(e.turn_counts(done + 1, n).tolist())
+            done += n
+        want = [series[t] for t in range(1, 10001)]
+        assert got == want
+        if size == 512:
+            # Local/count_test.go:43-49: period 2 beyond 10000 turns
+            e.step(2)
+            assert e.turn_counts(10001, 2).tolist() == [5567, 5565]
+
+
+def test_out_dir_secondary_goldens(gol):
+    """Verified-correct run outputs in the reference's Local/out/ (SURVEY §8c)."""
+    man = G.manifest()["out"]
+    labels = [1, 16, 25, 54, 58, 100, 159, 614, 641, 707, 763, 809, 1011, 1055, 1133, 1391,
+              1408, 2084, 2236, 2381, 3348, 8964, 10215]
+    want = {t: man[f"512x512x{t}.pgm"]["sha256"] for t in labels if f"512x512x{t}.pgm" in man}
+    assert len(want) >= 20
+    with _engine(gol, 512, 512) as e:
+        e.load(G.input_board(512))
+        for t in sorted(want):
+            e.step(t - e.turn)
+            assert hashlib.sha256(e.read_board().tobytes()).hexdigest() == want[t], t
+
+
+# ------------------------------------------------------- random vs oracle
+RANDOM_CASES = [
+    # (width, height, turns)   fast path: width % 128 == 0 and width >= 256
+    (256, 256, 7), (384, 100, 9), (512, 3, 5), (1024, 1, 4), (4096, 257, 13),
+    (5120, 64, 11), (8320, 40, 6),        # 8320: last tile has a single active lane
+    (16384, 96, 5),
+    # generic path
+    (2, 2, 5), (3, 7, 6), (16, 16, 9), (64, 64, 9), (65, 33, 8), (100, 50, 12),
+    (130, 20, 7), (200, 9, 10), (1000, 17, 6),
+]
+
+
+@pytest.mark.parametrize("w,h,turns", RANDOM_CASES)
+def test_random_vs_oracle(gol, oracle, w, h, turns):
+    seed = w * 7919 + h
+    with _engine(gol, w, h) as e:
+        e.fill_random(seed)
+        start = e.read_packed()
+        assert np.array_equal(start, oracle.gen_random(seed, w, h))
+        e.step(turns)
+        assert np.array_equal(e.read_packed(), oracle.bit_run(start, w, turns))
+
+
+@pytest.mark.parametrize("band", [1, 2, 3, 8, 61, 1000])
+def test_band_heights(gol, oracle, band):
+    w, h, turns, seed = 1024, 203, 6, 11
+    with _engine(gol, w, h, band_rows=band) as e:
+        e.fill_random(seed)
+        e.step(turns)
+        assert np.array_equal(e.read_packed(),
+                              oracle.bit_run(oracle.gen_random(seed, w, h), w, turns))
+
+
+def test_fast_equals_generic(gol):
+    w, h = 2048, 300
+    outs = []
+    for generic in (False, True):
+        with _engine(gol, w, h, force_generic=generic) as e:
+            assert e.info().fast_path == (0 if generic else 1)
+            e.fill_random(5)
+            e.step(17)
+            outs.append(e.read_packed())
+    assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("w,h", [(512, 64), (100, 37)])
+def test_count_every_turn_matches_oracle(gol, oracle, w, h):
+    with _engine(gol, w, h, count_every_turn=True) as e:
+        e.fill_random(9)
+        e.step(30)
+        got = e.turn_counts(1, 30)
+    _, want = oracle.bit_run(oracle.gen_random(9, w, h), w, 30, counts=True)
+    assert got.tolist() == want.astype(np.int64).tolist()
+
+
+# ----------------------------------------------------- non-binary quirk
+@pytest.mark.parametrize("w,h", [(16, 16), (256, 64), (130, 11)])
+def test_nonbinary_cells(gol, oracle, w, h):
+    """Bytes other than 0/255: dead as neighbours, centre -> 0 (SubServer/distributor.go:178-200);
+    Turns = 0 returns the bytes unchanged (the Server loop never runs)."""
+    rng = np.random.default_rng(w + h)
+    board = rng.choice(np.array([0, 255, 1, 7, 128, 254], dtype=np.uint8), size=(h, w),
+                       p=[0.45, 0.35, 0.05, 0.05, 0.05, 0.05])
+    with _engine(gol, w, h) as e:
+        e.load(board)
+        assert e.info().nonbinary_cells == int(((board != 0) & (board != 255)).sum())
+        assert np.array_equal(e.read_board(), board)
+        for t in (1, 2, 5):
+            e.step(t - e.turn)
+            assert np.array_equal(e.read_board(), oracle.ref_run(board, t, nsub=2, threads=3))
+
+
+# ------------------------------------------------------- strips in-process
+@pytest.mark.parametrize("n,K", [(1, 1), (2, 1), (2, 4), (3, 2), (4, 16), (7, 3), (8, 5)])
+@pytest.mark.parametrize("w", [512, 100])
+def test_strips_in_process(gol, oracle, n, K, w):
+    """Row strips with K-row halos exchanged every K turns == torus, for any N (the
+    reference's results are independent of len(SUB): Server/gol/distributor.go:106-116)."""
+    h, turns, seed = 120, 23, 4
+    board = oracle.unpack(oracle.gen_random(seed, w, h), w)
+    want = oracle.ref_run(board, turns, nsub=max(1, n), threads=2)
+    parts = gol.strip_split(h, n)
+    Kp = min(K, min(r for _, r in parts))
+    engs = [gol.Engine(w, h, device=0, row_offset=o, rows=r, halo=Kp) for o, r in parts]
+    try:
+        for e, (o, r) in zip(engs, parts):
+            e.load(gol.haloed_rows(board, o, r, Kp))
+        left = turns
+        while left:
+            if engs[0].halo_valid == 0:
+                for i, e in enumerate(engs):
+                    e.copy_halo_from_upper(engs[(i - 1) % n])
+                    e.copy_halo_from_lower(engs[(i + 1) % n])
+                for e in engs:
+                    e.halo_done()
+            m = min(left, engs[0].halo_valid)
+            for e in engs:
+                e.step(m)
+            left -= m
+        got = np.concatenate([e.read_board() for e in engs])
+        assert np.array_equal(got, want)
+        cells = np.concatenate([e.alive_cells() for e in engs])
+        assert np.array_equal(cells, oracle.ref_alive_cells(want))
+        assert sum(e.snapshot()[1] for e in engs) == int((want == 255).sum())
+    finally:
+        for e in engs:
+            e.close()
+
+
+def test_strip_rejects_exhausted_halo(gol):
+    e = gol.Engine(256, 64, device=0, row_offset=0, rows=32, halo=2)
+    try:
+        e.fill_random(1)
+        e.step(2)
+        with pytest.raises(Exception):
+            e.step(1)
+    finally:
+        e.close()
+
+
+def test_export_import_halo_torch(gol, oracle):
+    """The device-pointer halo path used over RCCL, exercised on one GPU."""
+    import torch
+    from gol.distributed import EngineStrip
+    w, h, n, K, turns = 512, 90, 3, 4, 14
+    dev = torch.device("cuda", 0)
+    board = oracle.unpack(oracle.gen_random(8, w, h), w)
+    parts = gol.strip_split(h, n)
+    strips = []
+    for o, r in parts:
+        e = gol.Engine(w, h, device=0, row_offset=o, rows=r, halo=K)
+        e.load(gol.haloed_rows(board, o, r, K))
+        strips.append(EngineStrip(e, dev))
+    left = turns
+    while left:
+        if strips[0].halo_valid == 0:
+            sent = [tuple(t.clone() for t in s.export_rows()) for s in strips]
+            for i, s in enumerate(strips):
+                s.import_rows(sent[(i - 1) % n][1], sent[(i + 1) % n][0])
+        m = min(left, strips[0].halo_valid)
+        for s in strips:
+            s.step(m)
+        left -= m
+    got = np.concatenate([s.engine.read_board() for s in strips])
+    assert np.array_equal(got, oracle.ref_run(board, turns, nsub=3, threads=2))
+    for s in strips:
+        s.engine.close()
+
+
+# --------------------------------------------------------- large boards
+def _digests():
+    path = os.path.join(G.GOLDEN, "large_digests.json")
+    with open(path) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("key", ["5120x5120_seed1_t1000", "16384x16384_seed2_t10000",
+                                 "65536x65536_seed3_t4", "65536x65536_seed3_t1000"])
+def test_large_board_digests(gol, key):
+    """BASELINE configs at full size vs oracle-computed digests (tests/golden/make_large_digests.py)."""
+    d = _digests()[key]
+    with _engine(gol, d["width"], d["height"]) as e:
+        e.fill_random(d["seed"])
+        e.step(d["turns"])
+        t, alive = e.snapshot()
+        assert alive == d["alive"]
+        words = e.read_packed()
+        assert hashlib.sha256(words.tobytes()).hexdigest() == d["sha256"]
+
+
+def test_65536_properties(gol, oracle):
+    """Size-independent checks at the headline size: torus translation invariance
+    (rolling the input by whole words commutes with the update) and 1-turn oracle parity."""
+    w = h = 65536
+    with _engine(gol, w, h) as e:
+        e.fill_random(3)
+        start = e.read_packed()
+        e.step(1)
+        one = e.read_packed()
+    assert np.array_equal(one, oracle.bit_run(start, w, 1, ncores=16))
+    rolled = np.roll(np.roll(start, 1000, axis=0), 3, axis=1)
+    with _engine(gol, w, h) as e:
+        e.load_packed(rolled)
+        e.step(1)
+        got = e.read_packed()
+    assert np.array_equal(got, np.roll(np.roll(one, 1000, axis=0), 3, axis=1))
