@@ -85,7 +85,9 @@ def main():
     from gol.distributed import DistStrip, EngineStrip, make_engine_strip
 
     W = H = a.size
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-default) stream shared by the engine, the events and RCCL
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     if world == 1:
         eng = gol.Engine(W, H, device=local, band_rows=a.band)
         eng.set_stream(stream.cuda_stream)
@@ -94,9 +96,8 @@ def main():
         rows_local = H
     else:
         eng = make_engine_strip(W, H, rank, world, a.halo, local, band_rows=a.band)
-        eng.set_stream(stream.cuda_stream)
         eng.fill_random(a.seed)
-        runner = DistStrip(EngineStrip(eng, dev), rank, world)
+        runner = DistStrip(EngineStrip(eng, dev, stream), rank, world)
         rows_local = eng.rows
     info = eng.info()
 

@@ -19,6 +19,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -43,6 +44,7 @@ struct gol_ctx {
     int nw = 0, pitch = 0, buf_rows = 0;
     bool fast = false;
     int band = 8;
+    int variant = golk::kVariantDefault;
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
     uint64_t *blocked = nullptr;
@@ -200,6 +202,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     c->buf_rows = cfg->rows + 2 * cfg->halo;
     c->fast = golk::fast_path_ok(cfg->width) && !(cfg->flags & GOL_FLAG_FORCE_GENERIC);
     c->band = cfg->band_rows > 0 ? cfg->band_rows : golk::auto_band(cfg->width, cfg->rows);
+    if (const char *v = getenv("GOL_STENCIL_VARIANT")) {   // A/B experiments only
+        const int k = atoi(v);
+        if (k >= 0 && k < golk::kVariantCount) c->variant = k;
+    }
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);
@@ -388,6 +394,7 @@ int gol_step(gol_ctx *c, int64_t turns)
     a.cnt_lo = own_lo(c);
     a.cnt_hi = own_hi(c);
     a.band = c->band;
+    a.variant = c->variant;
     for (int64_t t = 0; t < turns; ++t) {
         if (is_strip(c)) {
             // turn s (1-based) since the last exchange computes rows [s, buf_rows - s)

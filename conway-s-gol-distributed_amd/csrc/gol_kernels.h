@@ -23,7 +23,19 @@ struct StepArgs {
     int row_lo, row_hi;
     int cnt_lo, cnt_hi;                // rows whose outputs are counted
     int band;                          // rows per wavefront (fast) / per thread (generic)
+    int variant;                       // fast-path kernel variant (kVariant*)
 };
+
+// fast-path stencil variants (A/B-able in one process; kVariantDefault is shipped)
+enum : int {
+    kVariantWindow = 0,     // k_step_fast: 3-row window, 1 row in flight
+    kVariantRing2 = 1,      // k_step_ring<D=2>
+    kVariantRing3 = 2,      // k_step_ring<D=3>
+    kVariantRing3NT = 3,    // k_step_ring<D=3>, non-temporal stores
+    kVariantRing5 = 4,      // k_step_ring<D=5>
+    kVariantCount = 5,
+};
+extern const int kVariantDefault;
 
 bool fast_path_ok(int width);
 int auto_band(int width, int rows);

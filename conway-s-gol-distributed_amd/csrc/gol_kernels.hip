@@ -30,6 +30,8 @@
 // K4 k_pack / k_unpack — PGM bytes <-> bits, with the non-binary mask.
 #include "gol_kernels.h"
 
+#include <type_traits>
+
 namespace golk {
 
 // ------------------------------------------------------------------ helpers
@@ -196,6 +198,179 @@ __global__ __launch_bounds__(256) void k_step_fast(const uint64_t *__restrict__ 
         A = B; B = C; vc = vn;
         vn = vq; ln = lq; rn = rq;
     }
+    if (CNT) {
+        acc = wave_sum(acc);
+        if (lane == 0 && acc) atomicAdd(counts + (wv & (kShards - 1)), acc);
+    }
+}
+
+
+// ------------------------------------------- K1 v2: register ring, D rows in flight
+// Same algorithm as k_step_fast; the sliding window is a ring of Q = D + 3 row slots
+// (rows y-1, y, y+1 summed + D raw rows in flight) so each wavefront keeps D KiB of
+// loads outstanding, and the loop is unrolled by Q so every slot index is a
+// compile-time constant (no register rotation moves).  xor3 / majority are single
+// v_bitop3_b32 (truth tables 0x96 / 0xE8, symmetric in their operands).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// v_bitop3 truth-table index is (src0 << 2) | (src1 << 1) | src2 (checked against the
+// compiler's own lowering of a & ~b & ~c -> bitop3:0x10).
+template <int IMM>
+__device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(IMM));
+    return r;
+}
+
+struct Slot {
+    uint4 v;            // the lane's 4 dwords of this row
+    uint32_t hl, hr;    // tile-edge dwords (left of lane 0, right of the last lane)
+    uint32_t s0[4], s1[4];
+};
+
+typedef const __attribute__((address_space(4))) uint32_t *const_u32p;
+
+template <bool BLK, bool CNT, int D, bool NT>
+__global__ __launch_bounds__(256) void k_step_ring(const uint64_t *__restrict__ in,
+                                                   uint64_t *__restrict__ out,
+                                                   const uint64_t *__restrict__ blocked,
+                                                   unsigned long long *__restrict__ counts,
+                                                   StepArgs a, int ntx)
+{
+    constexpr int Q = D + 3;
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int tx = wv % ntx;
+    const int by = wv / ntx;
+    const int y0 = a.row_lo + by * a.band;
+    if (y0 >= a.row_hi) return;
+    const int y1 = min(y0 + a.band, a.row_hi);       // outputs [y0, y1); inputs [y0-1, y1]
+
+    const int nd = a.nw * 2;
+    const int tile0 = tx * (kTileWords * 2);
+    const int tile_end = min(tile0 + kTileWords * 2, nd);
+    const int d0 = tile0 + lane * 4;
+    const bool act = d0 < nd;
+    const int last_lane = ((tile_end - tile0) >> 2) - 1;
+    const int lidx = tile0 == 0 ? nd - 1 : tile0 - 1;
+    const int ridx = tile_end == nd ? 0 : tile_end;
+
+    const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in);
+    const_u32p in32s = (const_u32p)in32;   // wave-uniform edge dwords via the scalar path
+    uint32_t *out32 = reinterpret_cast<uint32_t *>(out);
+    const uint32_t *blk32 = reinterpret_cast<const uint32_t *>(blocked);
+    const size_t pitch32 = (size_t)a.pitch * 2;
+    const int M = a.modrows;
+    auto rowbase = [&](int r) -> size_t {
+        r = r < 0 ? r + M : (r >= M ? r - M : r);
+        return (size_t)r * pitch32;
+    };
+    auto load = [&](Slot &sl, int r) {
+        const size_t b = rowbase(r);
+        sl.v = act ? *reinterpret_cast<const uint4 *>(in32 + b + d0) : make_uint4(0, 0, 0, 0);
+        sl.hl = in32s[b + lidx];
+        sl.hr = in32s[b + ridx];
+    };
+    auto sums = [&](Slot &sl) {
+        const uint32_t L = dpp_from_lower(sl.hl, sl.v.w);
+        uint32_t R = dpp_from_upper(sl.hr, sl.v.x);
+        R = lane == last_lane ? sl.hr : R;
+        const uint32_t c[4] = {sl.v.x, sl.v.y, sl.v.z, sl.v.w};
+        uint32_t w[4], e[4];
+        w[0] = __builtin_amdgcn_alignbit(c[0], L, 31);
+        w[1] = __builtin_amdgcn_alignbit(c[1], c[0], 31);
+        w[2] = __builtin_amdgcn_alignbit(c[2], c[1], 31);
+        w[3] = __builtin_amdgcn_alignbit(c[3], c[2], 31);
+        e[0] = __builtin_amdgcn_alignbit(c[1], c[0], 1);
+        e[1] = __builtin_amdgcn_alignbit(c[2], c[1], 1);
+        e[2] = __builtin_amdgcn_alignbit(c[3], c[2], 1);
+        e[3] = __builtin_amdgcn_alignbit(R, c[3], 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            sl.s0[k] = xor3(w[k], c[k], e[k]);
+            sl.s1[k] = maj(w[k], c[k], e[k]);
+        }
+    };
+
+    Slot ring[Q];
+    // prologue: rows y0-1 .. y0+D into slots 0 .. D+1; sums of y0-1 and y0
+#pragma unroll
+    for (int k = 0; k < D + 2; ++k)
+        if (y0 - 1 + k <= y1) load(ring[k], y0 - 1 + k);
+    sums(ring[0]);
+    sums(ring[1]);
+    unsigned long long acc = 0;
+
+    // output row y uses slots (y-y0)%Q (row y-1), +1 (row y), +2 (row y+1); it prefetches
+    // row y+1+D into slot (y-y0+Q-1)%Q, which held row y-2.
+    auto body = [&](auto I, int y) {
+        constexpr int i = decltype(I)::value;
+        constexpr int sa = i % Q, sb = (i + 1) % Q, sc = (i + 2) % Q, sp = (i + Q - 1) % Q;
+        if (y + 1 + D <= y1) load(ring[sp], y + 1 + D);
+        sums(ring[sc]);
+        const uint32_t al[4] = {ring[sb].v.x, ring[sb].v.y, ring[sb].v.z, ring[sb].v.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t u0 = xor3(ring[sa].s0[k], ring[sb].s0[k], ring[sc].s0[k]);
+            const uint32_t u1 = maj(ring[sa].s0[k], ring[sb].s0[k], ring[sc].s0[k]);
+            const uint32_t v0 = xor3(ring[sa].s1[k], ring[sb].s1[k], ring[sc].s1[k]);
+            const uint32_t v1 = maj(ring[sa].s1[k], ring[sb].s1[k], ring[sc].s1[k]);
+            const uint32_t h1 = bitop3<0x14>(u1, v0, v1);      // (u1 ^ v0) & ~v1   : H == 1
+            const uint32_t h2 = bitop3<0x42>(u1, v0, v1);      // H == 2
+            const uint32_t x = bitop3<0x08>(u0, al[k], h2);     // ~u0 & alive & h2
+            o[k] = bitop3<0xea>(u0, h1, x);                     // (u0 & h1) | x
+        }
+        const size_t ob = rowbase(y);
+        if (BLK) {
+            const uint4 m = act ? *reinterpret_cast<const uint4 *>(blk32 + ob + d0)
+                                : make_uint4(0, 0, 0, 0);
+            o[0] &= ~m.x; o[1] &= ~m.y; o[2] &= ~m.z; o[3] &= ~m.w;
+        }
+        if (act) {
+            const uint4 ov = make_uint4(o[0], o[1], o[2], o[3]);
+            uint4 *dst = reinterpret_cast<uint4 *>(out32 + ob + d0);
+            if (NT) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 nv = {ov.x, ov.y, ov.z, ov.w};
+                __builtin_nontemporal_store(nv, reinterpret_cast<u32x4 *>(dst));
+            } else {
+                *dst = ov;
+            }
+        }
+        if (CNT && act && y >= a.cnt_lo && y < a.cnt_hi)
+            acc += __builtin_popcount(o[0]) + __builtin_popcount(o[1]) +
+                   __builtin_popcount(o[2]) + __builtin_popcount(o[3]);
+    };
+
+    int y = y0;
+    for (; y + Q <= y1; y += Q) {
+        body(std::integral_constant<int, 0>{}, y);
+        body(std::integral_constant<int, 1>{}, y + 1);
+        body(std::integral_constant<int, 2>{}, y + 2);
+        if constexpr (Q > 3) body(std::integral_constant<int, 3>{}, y + 3);
+        if constexpr (Q > 4) body(std::integral_constant<int, 4>{}, y + 4);
+        if constexpr (Q > 5) body(std::integral_constant<int, 5>{}, y + 5);
+        if constexpr (Q > 6) body(std::integral_constant<int, 6>{}, y + 6);
+    }
+    // remainder (< Q rows), continuing the ring phase from 0
+    if (y < y1) body(std::integral_constant<int, 0>{}, y);
+    if (y + 1 < y1) body(std::integral_constant<int, 1>{}, y + 1);
+    if (Q > 3 && y + 2 < y1) body(std::integral_constant<int, 2 % Q>{}, y + 2);
+    if (Q > 4 && y + 3 < y1) body(std::integral_constant<int, 3 % Q>{}, y + 3);
+    if (Q > 5 && y + 4 < y1) body(std::integral_constant<int, 4 % Q>{}, y + 4);
+    if (Q > 6 && y + 5 < y1) body(std::integral_constant<int, 5 % Q>{}, y + 5);
     if (CNT) {
         acc = wave_sum(acc);
         if (lane == 0 && acc) atomicAdd(counts + (wv & (kShards - 1)), acc);
@@ -429,6 +604,44 @@ int auto_band(int width, int rows)
     return (int)b;
 }
 
+const int kVariantDefault = kVariantRing3;
+
+template <bool BLK, bool CNT>
+static void launch_fast(const StepArgs &a, int ntx, int blocks, hipStream_t s)
+{
+    switch (a.variant) {
+    case kVariantWindow:
+        hipLaunchKernelGGL((k_step_fast<BLK, CNT>), dim3(blocks), dim3(256), 0, s, a.in, a.out,
+                           a.blocked, a.counts, a, ntx);
+        break;
+    case kVariantRing2:
+        hipLaunchKernelGGL((k_step_ring<BLK, CNT, 2, false>), dim3(blocks), dim3(256), 0, s,
+                           a.in, a.out, a.blocked, a.counts, a, ntx);
+        break;
+    case kVariantRing3NT:
+        hipLaunchKernelGGL((k_step_ring<BLK, CNT, 3, true>), dim3(blocks), dim3(256), 0, s,
+                           a.in, a.out, a.blocked, a.counts, a, ntx);
+        break;
+    case kVariantRing5:
+        hipLaunchKernelGGL((k_step_ring<BLK, CNT, 5, false>), dim3(blocks), dim3(256), 0, s,
+                           a.in, a.out, a.blocked, a.counts, a, ntx);
+        break;
+    case kVariantRing3:
+    default:
+        hipLaunchKernelGGL((k_step_ring<BLK, CNT, 3, false>), dim3(blocks), dim3(256), 0, s,
+                           a.in, a.out, a.blocked, a.counts, a, ntx);
+        break;
+    }
+}
+
+template <bool BLK, bool CNT>
+static void launch_generic(const StepArgs &a, hipStream_t s)
+{
+    const int g = grid_for((long long)(a.row_hi - a.row_lo) * a.nw);
+    hipLaunchKernelGGL((k_step_generic<BLK, CNT>), dim3(g), dim3(256), 0, s, a.in, a.out,
+                       a.blocked, a.counts, a);
+}
+
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
 {
     if (a.row_hi <= a.row_lo) return hipSuccess;
@@ -438,32 +651,15 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
         const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
         const long long nwaves = (long long)ntx * nbands;
         const int blocks = (int)((nwaves + 3) / 4);
-        if (blk && cnt)
-            hipLaunchKernelGGL((k_step_fast<true, true>), dim3(blocks), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a, ntx);
-        else if (blk)
-            hipLaunchKernelGGL((k_step_fast<true, false>), dim3(blocks), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a, ntx);
-        else if (cnt)
-            hipLaunchKernelGGL((k_step_fast<false, true>), dim3(blocks), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a, ntx);
-        else
-            hipLaunchKernelGGL((k_step_fast<false, false>), dim3(blocks), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a, ntx);
+        if (blk && cnt) launch_fast<true, true>(a, ntx, blocks, s);
+        else if (blk) launch_fast<true, false>(a, ntx, blocks, s);
+        else if (cnt) launch_fast<false, true>(a, ntx, blocks, s);
+        else launch_fast<false, false>(a, ntx, blocks, s);
     } else {
-        const int g = grid_for((long long)(a.row_hi - a.row_lo) * a.nw);
-        if (blk && cnt)
-            hipLaunchKernelGGL((k_step_generic<true, true>), dim3(g), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a);
-        else if (blk)
-            hipLaunchKernelGGL((k_step_generic<true, false>), dim3(g), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a);
-        else if (cnt)
-            hipLaunchKernelGGL((k_step_generic<false, true>), dim3(g), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a);
-        else
-            hipLaunchKernelGGL((k_step_generic<false, false>), dim3(g), dim3(256), 0, s, a.in,
-                               a.out, a.blocked, a.counts, a);
+        if (blk && cnt) launch_generic<true, true>(a, s);
+        else if (blk) launch_generic<true, false>(a, s);
+        else if (cnt) launch_generic<false, true>(a, s);
+        else launch_generic<false, false>(a, s);
     }
     return hipGetLastError();
 }

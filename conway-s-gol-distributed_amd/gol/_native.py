@@ -135,6 +135,14 @@ def lib() -> ctypes.CDLL:
     """Load libgolamd.so (raises if it has not been built: no CPU fallback)."""
     global _lib
     if _lib is None:
+        # torch (when present) ships its own libamdhip64 whose NEEDED name differs from
+        # ours (libamdhip64.so vs .so.7); loading ours first would put two HIP runtimes
+        # in the process and torch would see no GPU.  Loading torch first makes our
+        # libamdhip64.so.7 dependency resolve to torch's already-loaded runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(
                 f"native engine {LIB_PATH} is missing; build it with "

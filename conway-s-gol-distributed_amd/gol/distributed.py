@@ -27,11 +27,17 @@ TAG_DOWN = 18    # rows travelling to the lower neighbour (they become its top h
 
 
 class EngineStrip:
-    """Adapter exposing an Engine strip to the exchange loop with torch tensors."""
+    """Adapter exposing an Engine strip to the exchange loop with torch tensors.
 
-    def __init__(self, engine: Engine, device: torch.device):
+    The engine and the halo messages share one dedicated torch stream, so the RCCL
+    send/recv that torch enqueues are ordered after the engine's turns and before its
+    next ones without host synchronisation."""
+
+    def __init__(self, engine: Engine, device: torch.device, stream=None):
         self.engine = engine
         self.device = device
+        self.stream = stream if stream is not None else torch.cuda.Stream(device)
+        engine.set_stream(self.stream.cuda_stream)
         K, nw = engine.halo, engine.words_per_row
         mk = lambda: torch.empty((K, nw), dtype=torch.int64, device=device)  # noqa: E731
         self.top_send, self.bot_send, self.top_recv, self.bot_recv = mk(), mk(), mk(), mk()
@@ -43,8 +49,11 @@ class EngineStrip:
     def step(self, n: int):
         self.engine.step(n)
 
+    def stream_context(self):
+        return torch.cuda.stream(self.stream)
+
     def export_rows(self):
-        s = torch.cuda.current_stream(self.device).cuda_stream
+        s = self.stream.cuda_stream
         self.engine.export_halo(self.top_send.data_ptr(), self.bot_send.data_ptr(), s)
         return self.top_send, self.bot_send
 
@@ -52,7 +61,7 @@ class EngineStrip:
         return self.top_recv, self.bot_recv
 
     def import_rows(self, top, bottom):
-        s = torch.cuda.current_stream(self.device).cuda_stream
+        s = self.stream.cuda_stream
         if top.device != self.device:
             self.top_recv.copy_(top, non_blocking=True)
             self.bot_recv.copy_(bottom, non_blocking=True)
@@ -74,6 +83,13 @@ class DistStrip:
         self.exchanges = 0
 
     def exchange(self):
+        ctx = getattr(self.strip, "stream_context", None)
+        if ctx is None:
+            return self._exchange()
+        with ctx():
+            return self._exchange()
+
+    def _exchange(self):
         top, bot = self.strip.export_rows()
         top_recv, bot_recv = self.strip.recv_buffers()
         if self.stage_on_host:

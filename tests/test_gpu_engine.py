@@ -117,6 +117,20 @@ def test_band_heights(gol, oracle, band):
                               oracle.bit_run(oracle.gen_random(seed, w, h), w, turns))
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("w,h,band", [(8320, 41, 5), (1024, 203, 7), (4096, 64, 64), (512, 37, 1000)])
+def test_stencil_variants(gol, oracle, monkeypatch, variant, w, h, band):
+    """Every fast-path kernel variant (A/B candidates) is bit-exact, incl. ragged bands."""
+    monkeypatch.setenv("GOL_STENCIL_VARIANT", str(variant))
+    with _engine(gol, w, h, band_rows=band, count_every_turn=True) as e:
+        e.fill_random(variant + 100)
+        e.step(9)
+        got, counts = e.read_packed(), e.turn_counts(1, 9)
+    want, wc = oracle.bit_run(oracle.gen_random(variant + 100, w, h), w, 9, counts=True)
+    assert np.array_equal(got, want)
+    assert counts.tolist() == wc.astype(np.int64).tolist()
+
+
 def test_fast_equals_generic(gol):
     w, h = 2048, 300
     outs = []

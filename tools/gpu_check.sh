@@ -1,0 +1,23 @@
+#!/bin/bash
+# One GPU-box pass: engine parity, run-driver parity, a short bench.
+# Each step has its own time limit; a crash / fault / timeout stops the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+run() {  # name seconds cmd...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    engine) run t_engine 500 python -u -m pytest tests/test_gpu_engine.py -v --timeout 150 --timeout-method thread ;;
+    run)    run t_run 400 python -u -m pytest tests/test_gpu_run.py -v --timeout 120 --timeout-method thread ;;
+    smoke)  run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  run bench 300 python -u bench.py --steps 200 --no-cpu-baseline ;;
+    benchfull) run benchfull 400 python -u bench.py ;;
+  esac
+done
