@@ -33,7 +33,9 @@ enum : int {
     kVariantRing3 = 2,      // k_step_ring<D=3>
     kVariantRing3NT = 3,    // k_step_ring<D=3>, non-temporal stores
     kVariantRing5 = 4,      // k_step_ring<D=5>
-    kVariantCount = 5,
+    kVariantRing7 = 5,      // k_step_ring<D=7>
+    kVariantRing5NT = 6,    // k_step_ring<D=5>, non-temporal stores
+    kVariantCount = 7,
 };
 extern const int kVariantDefault;
 

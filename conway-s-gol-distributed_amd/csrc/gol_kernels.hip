@@ -233,6 +233,12 @@ __device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
+template <typename F, int... Is>
+__device__ __forceinline__ void unroll_seq(std::integer_sequence<int, Is...>, F &&f)
+{
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+
 struct Slot {
     uint4 v;            // the lane's 4 dwords of this row
     uint32_t hl, hr;    // tile-edge dwords (left of lane 0, right of the last lane)
@@ -355,22 +361,12 @@ __global__ __launch_bounds__(256) void k_step_ring(const uint64_t *__restrict__ 
     };
 
     int y = y0;
-    for (; y + Q <= y1; y += Q) {
-        body(std::integral_constant<int, 0>{}, y);
-        body(std::integral_constant<int, 1>{}, y + 1);
-        body(std::integral_constant<int, 2>{}, y + 2);
-        if constexpr (Q > 3) body(std::integral_constant<int, 3>{}, y + 3);
-        if constexpr (Q > 4) body(std::integral_constant<int, 4>{}, y + 4);
-        if constexpr (Q > 5) body(std::integral_constant<int, 5>{}, y + 5);
-        if constexpr (Q > 6) body(std::integral_constant<int, 6>{}, y + 6);
-    }
+    for (; y + Q <= y1; y += Q)
+        unroll_seq(std::make_integer_sequence<int, Q>{}, [&](auto I) { body(I, y + I); });
     // remainder (< Q rows), continuing the ring phase from 0
-    if (y < y1) body(std::integral_constant<int, 0>{}, y);
-    if (y + 1 < y1) body(std::integral_constant<int, 1>{}, y + 1);
-    if (Q > 3 && y + 2 < y1) body(std::integral_constant<int, 2 % Q>{}, y + 2);
-    if (Q > 4 && y + 3 < y1) body(std::integral_constant<int, 3 % Q>{}, y + 3);
-    if (Q > 5 && y + 4 < y1) body(std::integral_constant<int, 4 % Q>{}, y + 4);
-    if (Q > 6 && y + 5 < y1) body(std::integral_constant<int, 5 % Q>{}, y + 5);
+    unroll_seq(std::make_integer_sequence<int, Q - 1>{}, [&](auto I) {
+        if (y + I < y1) body(I, y + I);
+    });
     if (CNT) {
         acc = wave_sum(acc);
         if (lane == 0 && acc) atomicAdd(counts + (wv & (kShards - 1)), acc);
@@ -596,11 +592,12 @@ int auto_band(int width, int rows)
     const int nw = (width + 63) / 64;
     const long long ntx = fast_path_ok(width) ? (nw + kTileWords - 1) / kTileWords : 1;
     const long long row_tiles = (long long)rows * ntx;
-    // aim for ~8192 wavefronts (32 per CU on 256 CUs); keep bands >= 8 rows so
-    // the 2 halo rows per band stay a small re-read, <= 128 to bound the tail.
-    long long b = row_tiles / 8192;
+    // Measured on MI355X (tools/sweep.py): short bands win -- 16 rows at 65536^2
+    // (32768 wavefronts, ~8 residency rounds at 4 waves/SIMD), 8 rows at 16384^2.
+    // The 2 halo rows per band are L2/MALL re-reads, not HBM traffic.
+    long long b = row_tiles / 32768;
     if (b < 8) b = 8;
-    if (b > 128) b = 128;
+    if (b > 64) b = 64;
     return (int)b;
 }
 
@@ -624,6 +621,14 @@ static void launch_fast(const StepArgs &a, int ntx, int blocks, hipStream_t s)
         break;
     case kVariantRing5:
         hipLaunchKernelGGL((k_step_ring<BLK, CNT, 5, false>), dim3(blocks), dim3(256), 0, s,
+                           a.in, a.out, a.blocked, a.counts, a, ntx);
+        break;
+    case kVariantRing7:
+        hipLaunchKernelGGL((k_step_ring<BLK, CNT, 7, false>), dim3(blocks), dim3(256), 0, s,
+                           a.in, a.out, a.blocked, a.counts, a, ntx);
+        break;
+    case kVariantRing5NT:
+        hipLaunchKernelGGL((k_step_ring<BLK, CNT, 5, true>), dim3(blocks), dim3(256), 0, s,
                            a.in, a.out, a.blocked, a.counts, a, ntx);
         break;
     case kVariantRing3:

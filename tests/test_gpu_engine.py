@@ -117,7 +117,7 @@ def test_band_heights(gol, oracle, band):
                               oracle.bit_run(oracle.gen_random(seed, w, h), w, turns))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("w,h,band", [(8320, 41, 5), (1024, 203, 7), (4096, 64, 64), (512, 37, 1000)])
 def test_stencil_variants(gol, oracle, monkeypatch, variant, w, h, band):
     """Every fast-path kernel variant (A/B candidates) is bit-exact, incl. ragged bands."""
