@@ -53,6 +53,19 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(size, k):
+    """HBM traffic per launch of the stencil from the newest committed rocprofv3 PMC pass
+    for this board size and k (profiles/rNN_k{k}_{size}_summary.json, written by
+    tools/profile.sh + tools/summarize_profile.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_k{k}_{size}_summary.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(size, seed, turns, cores):
     """oracle/refcpu.c (literal restatement of the reference's Server/SubServer CPU path,
     4 sub-servers as in the reference's default SUB list, Threads = cores) on the same
@@ -128,6 +141,7 @@ def main():
     # per-launch average of the stencil on this rank's stream (one launch per turn)
     cells_local = rows_local * W
     launch_us = gpu_ms * 1e3 / a.steps
+    traffic, traffic_src = pmc_traffic(W, 1)
     achieved = BYTES_PER_CELL_UPDATE * cells_local / (launch_us * 1e-6) / 1e9
     gcups = W * H * a.steps / wall / 1e9
 
@@ -153,7 +167,8 @@ def main():
                        "temporal_blocking_k": 1},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "k_step_fast",
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "k_step_ring<D=3>",
                          "launch_us": round(launch_us, 2),
                          "bytes_per_launch": int(BYTES_PER_CELL_UPDATE * cells_local)},
             "cpu_baseline": None,

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run (gpurun_out/prof) into profiles/<tag>_*.{csv,json}.
+
+traffic per launch = (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 bytes for the stencil kernel:
+FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads exactly half of a wide
+(16 B/lane) coalesced stream (MI355X_MICROARCH.md, HBM section), so it is doubled;
+WRITE_SIZE is exact for 16-B-per-lane stores.  Infinity-Cache hits are included in
+both, so this is fabric traffic out of the XCD L2s (an upper bound on HBM bytes)."""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(tag, src=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_step"):
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"),
+                os.path.join(out, f"{tag}_kernel_stats.csv"))
+    stats = list(csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))))
+    top = max(stats, key=lambda r: float(r["TotalDurationNs"]))
+    res = {"kernel": top["Name"], "calls": int(top["Calls"]),
+           "avg_ns": float(top["AverageNs"]), "min_ns": float(top["MinNs"]),
+           "max_ns": float(top["MaxNs"]), "share_pct": float(top["Percentage"])}
+    for name, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        p = os.path.join(src, name, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        rows = [r for r in csv.DictReader(open(p))
+                if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+        res[counter + "_kib_median"] = statistics.median(float(r["Counter_Value"]) for r in rows)
+        res[counter + "_launches"] = len(rows)
+    if "FETCH_SIZE_kib_median" in res and "WRITE_SIZE_kib_median" in res:
+        rd = res["FETCH_SIZE_kib_median"] * 2 * 1024
+        wr = res["WRITE_SIZE_kib_median"] * 1024
+        res["read_bytes_per_launch"] = rd
+        res["write_bytes_per_launch"] = wr
+        res["traffic_bytes_per_launch"] = rd + wr
+    with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
