@@ -35,6 +35,7 @@ namespace {
 
 constexpr int kRing = 4096;                 // per-turn count ring (turn t -> slot t % kRing)
 constexpr size_t kStagingBytes = 256u << 20;  // byte staging chunk for load / read
+constexpr int kDefaultTurnsPerLaunch = 1;     // temporal blocking off unless configured
 
 }  // namespace
 
@@ -45,6 +46,7 @@ struct gol_ctx {
     bool fast = false;
     int band = 8;
     int variant = golk::kVariantDefault;
+    int tpl = 1;                             // turns per stencil launch (temporal blocking)
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
     uint64_t *blocked = nullptr;
@@ -206,6 +208,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         const int k = atoi(v);
         if (k >= 0 && k < golk::kVariantCount) c->variant = k;
     }
+    c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : kDefaultTurnsPerLaunch;
+    if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
+    c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
+    if (!c->fast) c->tpl = 1;
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);
@@ -268,6 +274,7 @@ int gol_get_info(gol_ctx *c, gol_info *info)
     info->fast_path = c->fast ? 1 : 0;
     info->band_rows = c->band;
     info->halo_valid = c->halo_valid;
+    info->turns_per_launch = c->tpl;
     info->device = c->device;
     info->turn = c->turn;
     info->nonbinary_cells = c->nonbinary;
@@ -395,39 +402,52 @@ int gol_step(gol_ctx *c, int64_t turns)
     a.cnt_hi = own_hi(c);
     a.band = c->band;
     a.variant = c->variant;
-    for (int64_t t = 0; t < turns; ++t) {
+    for (int64_t t = 0; t < turns;) {
+        // temporal blocking: fuse k turns into one pass when nothing needs per-turn output
+        int k = 1;
+        if (c->tpl > 1 && !cnt && !c->blocked_pending) {
+            int64_t room = turns - t;
+            if (is_strip(c)) room = std::min<int64_t>(room, c->halo_valid);
+            k = (int)std::min<int64_t>(room, c->tpl);
+            if (k == 7) k = 6;                     // supported depths: 2..6, 8
+            if (!golk::multi_ok(c->cfg.width, k)) k = 1;
+        }
+        // rows computed: torus -> all; strip -> [s, buf_rows - s) after turn s since exchange
+        const int s0 = is_strip(c) ? c->cfg.halo - c->halo_valid : 0;
         if (is_strip(c)) {
-            // turn s (1-based) since the last exchange computes rows [s, buf_rows - s)
-            const int s = c->cfg.halo - c->halo_valid + 1;
-            a.row_lo = s;
-            a.row_hi = c->buf_rows - s;
+            a.row_lo = s0 + k;
+            a.row_hi = c->buf_rows - s0 - k;
         } else {
             a.row_lo = 0;
             a.row_hi = c->buf_rows;
         }
         a.in = c->board[c->cur];
         a.out = c->board[c->cur ^ 1];
-        a.blocked = c->blocked_pending ? c->blocked : nullptr;
-        a.counts = nullptr;
-        if (cnt) {
-            const long long next_turn = c->turn + 1;
-            const size_t slot = (size_t)(next_turn % kRing);
-            if (t % kRing == 0) {
-                // zero the slots of the next min(turns - t, kRing) turns (ring may wrap once)
-                const size_t nslots = (size_t)std::min<int64_t>(turns - t, kRing);
-                const size_t first = std::min(nslots, (size_t)kRing - slot);
-                HIP_OR_FAIL(c, hipMemsetAsync(c->counts + slot * kShards, 0,
-                                              first * kShards * 8, c->stream));
-                if (nslots > first)
-                    HIP_OR_FAIL(c, hipMemsetAsync(c->counts, 0, (nslots - first) * kShards * 8,
-                                                  c->stream));
+        if (k > 1) {
+            a.blocked = nullptr;
+            a.counts = nullptr;
+            HIP_OR_FAIL(c, golk::launch_step_multi(a, k, c->stream));
+        } else {
+            a.blocked = c->blocked_pending ? c->blocked : nullptr;
+            a.counts = nullptr;
+            if (cnt) {
+                const long long next_turn = c->turn + 1;
+                const size_t slot = (size_t)(next_turn % kRing);
+                if (slot == 0 || t == 0) {
+                    // zero the slots of the next min(turns - t, kRing - slot) turns
+                    const size_t nslots =
+                        (size_t)std::min<int64_t>(turns - t, (int64_t)(kRing - slot));
+                    HIP_OR_FAIL(c, hipMemsetAsync(c->counts + slot * kShards, 0,
+                                                  nslots * kShards * 8, c->stream));
+                }
+                a.counts = c->counts + slot * kShards;
             }
-            a.counts = c->counts + slot * kShards;
+            HIP_OR_FAIL(c, golk::launch_step(a, c->fast, c->stream));
         }
-        HIP_OR_FAIL(c, golk::launch_step(a, c->fast, c->stream));
         c->cur ^= 1;
-        c->turn += 1;
-        if (is_strip(c)) c->halo_valid -= 1;
+        c->turn += k;
+        t += k;
+        if (is_strip(c)) c->halo_valid -= k;
         if (c->blocked_pending) {
             // every cell is 0/255 after the first turn; the mask is dead from here on
             c->blocked_pending = false;

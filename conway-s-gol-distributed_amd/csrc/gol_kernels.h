@@ -40,6 +40,13 @@ enum : int {
 extern const int kVariantDefault;
 
 bool fast_path_ok(int width);
+
+// K turns per launch (temporal blocking): outputs rows [row_lo, row_hi) after `turns`
+// turns, reading rows [row_lo - turns, row_hi + turns) (mod modrows).  No blocked mask,
+// no counts.  turns in {2, 3, 4, 5, 6, 8}.
+constexpr int kMaxTurnsPerLaunch = 8;
+bool multi_ok(int width, int turns);
+hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);
 

@@ -373,6 +373,125 @@ __global__ __launch_bounds__(256) void k_step_ring(const uint64_t *__restrict__ 
     }
 }
 
+
+// ------------------------------------- K1m: K turns per launch (temporal blocking)
+// A wavefront owns a tile of 128 words (64 lanes x 2 words) whose first and last lane
+// are halo lanes: only lanes 1..62 (124 words) are stored, tiles advance by 124 words.
+// The tile edges are never loaded: DPP brings zeros into lane 0 / past the last lane,
+// and that error travels one cell per turn, so after K <= 64 turns it is still inside
+// the halo lanes (128 cells each).  Vertically, a band of `band` output rows reads
+// input rows [y0-K, y1+K) once; stage j (j = 0..K-1) turns its input row stream into
+// the stream of turn t+j+1 rows one row later, all in registers.  HBM traffic per
+// launch is one read + one write of the board for K turns: 0.25/K B per cell-update.
+constexpr int kMultiStride = kTileWords - 4;   // 124 stored words per tile
+
+template <int K>
+__global__ __launch_bounds__(256) void k_step_multi(const uint64_t *__restrict__ in,
+                                                    uint64_t *__restrict__ out, StepArgs a,
+                                                    int ntx)
+{
+    const int lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int tx = wv % ntx;
+    const int by = wv / ntx;
+    const int y0 = a.row_lo + by * a.band;
+    if (y0 >= a.row_hi) return;
+    const int y1 = min(y0 + a.band, a.row_hi);         // outputs [y0, y1)
+
+    const int nw = a.nw;
+    const int t0 = tx * kMultiStride;                  // first stored word
+    const int t1 = min(t0 + kMultiStride, nw);         // end of stored words
+    const int last = (t1 - t0) / 2 + 1;                // right halo lane
+    const bool act = lane <= last;
+    const bool st = lane >= 1 && lane < last;
+    int w = t0 - 2 + 2 * lane;                         // lane's first word (torus wrap)
+    w = w < 0 ? w + nw : (w >= nw ? w - nw : w);
+    const size_t pitch32 = (size_t)a.pitch * 2;
+    const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in) + 2 * (size_t)w;
+    uint32_t *out32 = reinterpret_cast<uint32_t *>(out) + 2 * (size_t)w;
+    const int M = a.modrows;
+    auto rowoff = [&](int r) -> size_t {     // r in [-K, M + K): may wrap more than once
+        while (r < 0) r += M;
+        while (r >= M) r -= M;
+        return (size_t)r * pitch32;
+    };
+    auto load = [&](int r) -> uint4 {
+        return act ? *reinterpret_cast<const uint4 *>(in32 + rowoff(r)) : make_uint4(0, 0, 0, 0);
+    };
+    auto sums = [&](const uint4 &v, uint32_t (&s0)[4], uint32_t (&s1)[4]) {
+        const uint32_t L = dpp_from_lower(0u, v.w);
+        const uint32_t R = dpp_from_upper(0u, v.x);
+        const uint32_t c[4] = {v.x, v.y, v.z, v.w};
+        uint32_t wv_[4], e[4];
+        wv_[0] = __builtin_amdgcn_alignbit(c[0], L, 31);
+        wv_[1] = __builtin_amdgcn_alignbit(c[1], c[0], 31);
+        wv_[2] = __builtin_amdgcn_alignbit(c[2], c[1], 31);
+        wv_[3] = __builtin_amdgcn_alignbit(c[3], c[2], 31);
+        e[0] = __builtin_amdgcn_alignbit(c[1], c[0], 1);
+        e[1] = __builtin_amdgcn_alignbit(c[2], c[1], 1);
+        e[2] = __builtin_amdgcn_alignbit(c[3], c[2], 1);
+        e[3] = __builtin_amdgcn_alignbit(R, c[3], 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s0[k] = xor3(wv_[k], c[k], e[k]);
+            s1[k] = maj(wv_[k], c[k], e[k]);
+        }
+    };
+
+    // per stage: ring of 3 row sums and 3 raw input rows (phase = step % 3)
+    uint32_t S0[K][3][4], S1[K][3][4];
+    uint4 X[K][3];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            X[j][p] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) S0[j][p][k] = S1[j][p][k] = 0;
+        }
+    uint4 raw[3];
+    const int r_first = y0 - K, r_end = y1 + K;         // input rows [r_first, r_end)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) raw[p] = (r_first + p < r_end) ? load(r_first + p) : make_uint4(0, 0, 0, 0);
+
+    auto step = [&](auto I, int r) {                    // r = input row of this step
+        constexpr int i = decltype(I)::value;
+        constexpr int pn = i % 3, p1 = (i + 2) % 3, p2 = (i + 1) % 3;
+        uint4 x = raw[pn];
+        if (r + 3 < r_end) raw[pn] = load(r + 3);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            sums(x, S0[j][pn], S1[j][pn]);
+            X[j][pn] = x;
+            const uint32_t al[4] = {X[j][p1].x, X[j][p1].y, X[j][p1].z, X[j][p1].w};
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t u0 = xor3(S0[j][p2][k], S0[j][p1][k], S0[j][pn][k]);
+                const uint32_t u1 = maj(S0[j][p2][k], S0[j][p1][k], S0[j][pn][k]);
+                const uint32_t v0 = xor3(S1[j][p2][k], S1[j][p1][k], S1[j][pn][k]);
+                const uint32_t v1 = maj(S1[j][p2][k], S1[j][p1][k], S1[j][pn][k]);
+                const uint32_t h1 = bitop3<0x14>(u1, v0, v1);
+                const uint32_t h2 = bitop3<0x42>(u1, v0, v1);
+                const uint32_t xx = bitop3<0x08>(u0, al[k], h2);
+                o[k] = bitop3<0xea>(u0, h1, xx);
+            }
+            x = make_uint4(o[0], o[1], o[2], o[3]);     // stage j output = row r-1-j
+        }
+        const int ry = r - K;                            // final output row
+        if (st && ry >= y0) *reinterpret_cast<uint4 *>(out32 + rowoff(ry)) = x;
+    };
+
+    int r = r_first;
+    for (; r + 3 <= r_end; r += 3) {
+        step(std::integral_constant<int, 0>{}, r);
+        step(std::integral_constant<int, 1>{}, r + 1);
+        step(std::integral_constant<int, 2>{}, r + 2);
+    }
+    if (r < r_end) step(std::integral_constant<int, 0>{}, r);
+    if (r + 1 < r_end) step(std::integral_constant<int, 1>{}, r + 1);
+}
+
 // ---------------------------------------------------- K1g: generic stencil
 __device__ __forceinline__ uint64_t west_word(const uint64_t *row, int j, int nw, int nb)
 {
@@ -666,6 +785,37 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
         else if (cnt) launch_generic<false, true>(a, s);
         else launch_generic<false, false>(a, s);
     }
+    return hipGetLastError();
+}
+
+bool multi_ok(int width, int turns)
+{
+    return fast_path_ok(width) && turns >= 2 && turns <= kMaxTurnsPerLaunch;
+}
+
+hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s)
+{
+    if (a.row_hi <= a.row_lo) return hipSuccess;
+    const int ntx = (a.nw + kMultiStride - 1) / kMultiStride;
+    const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
+    const long long nwaves = (long long)ntx * nbands;
+    const int blocks = (int)((nwaves + 3) / 4);
+#define GOL_MULTI(K)                                                                          \
+    case K:                                                                                   \
+        hipLaunchKernelGGL((k_step_multi<K>), dim3(blocks), dim3(256), 0, s, a.in, a.out, a,  \
+                           ntx);                                                              \
+        break;
+    switch (turns) {
+        GOL_MULTI(2)
+        GOL_MULTI(3)
+        GOL_MULTI(4)
+        GOL_MULTI(5)
+        GOL_MULTI(6)
+        GOL_MULTI(8)
+    default:
+        return hipErrorInvalidValue;
+    }
+#undef GOL_MULTI
     return hipGetLastError();
 }
 

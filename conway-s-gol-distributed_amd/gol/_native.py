@@ -46,7 +46,8 @@ class gol_config(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("device", ctypes.c_int32), ("row_offset", ctypes.c_int32),
                 ("rows", ctypes.c_int32), ("halo", ctypes.c_int32),
-                ("flags", ctypes.c_uint32), ("band_rows", ctypes.c_int32)]
+                ("flags", ctypes.c_uint32), ("band_rows", ctypes.c_int32),
+                ("turns_per_launch", ctypes.c_int32)]
 
 
 class gol_info(ctypes.Structure):
@@ -55,7 +56,8 @@ class gol_info(ctypes.Structure):
                 ("halo", ctypes.c_int32), ("words_per_row", ctypes.c_int32),
                 ("pitch_words", ctypes.c_int32), ("buffer_rows", ctypes.c_int32),
                 ("fast_path", ctypes.c_int32), ("band_rows", ctypes.c_int32),
-                ("halo_valid", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("halo_valid", ctypes.c_int32), ("turns_per_launch", ctypes.c_int32),
+                ("device", ctypes.c_int32),
                 ("turn", ctypes.c_int64), ("nonbinary_cells", ctypes.c_int64)]
 
 

@@ -18,7 +18,7 @@ from . import _native as N
 class Engine:
     def __init__(self, width: int, height: int, *, device: int = -1, row_offset: int = 0,
                  rows: int | None = None, halo: int = 0, count_every_turn: bool = False,
-                 force_generic: bool = False, band_rows: int = 0):
+                 force_generic: bool = False, band_rows: int = 0, turns_per_launch: int = 0):
         L = N.lib()
         cfg = N.gol_config()
         cfg.width, cfg.height = int(width), int(height)
@@ -29,6 +29,7 @@ class Engine:
         cfg.flags = ((N.GOL_FLAG_COUNT_EVERY_TURN if count_every_turn else 0) |
                      (N.GOL_FLAG_FORCE_GENERIC if force_generic else 0))
         cfg.band_rows = int(band_rows)
+        cfg.turns_per_launch = int(turns_per_launch)
         h = ctypes.c_void_p()
         N.check(L.gol_create_ex(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

@@ -71,6 +71,8 @@ typedef struct gol_config {
     int32_t  halo;        /* strip mode: halo depth K in rows (1 <= K <= rows)            */
     uint32_t flags;       /* GOL_FLAG_*                                                   */
     int32_t  band_rows;   /* rows per wavefront band in the stencil; 0 = auto             */
+    int32_t  turns_per_launch; /* temporal blocking: turns fused per stencil pass (1 = off;
+                                  0 = default); results are identical for every value   */
 } gol_config;
 
 typedef struct gol_info {
@@ -81,6 +83,7 @@ typedef struct gol_info {
     int32_t  fast_path;         /* 1 = the LDS-free DPP stencil (width % 128 == 0, >= 256) */
     int32_t  band_rows;         /* effective band height                              */
     int32_t  halo_valid;        /* strip mode: turns left before the next exchange    */
+    int32_t  turns_per_launch;  /* effective temporal-blocking depth                   */
     int32_t  device;
     int64_t  turn;              /* completed turns since load                          */
     int64_t  nonbinary_cells;   /* cells that were neither 0 nor 255 at load           */

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="0,1,2,3,4")
     ap.add_argument("--bands", default="0,32,64,128")
+    ap.add_argument("--tpl", default="1", help="turns per launch values")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     W, H = a.size, a.height or a.size
@@ -31,12 +32,13 @@ def main():
     engines = {}
     for v in [int(x) for x in a.variants.split(",")]:
         for b in [int(x) for x in a.bands.split(",")]:
-            os.environ["GOL_STENCIL_VARIANT"] = str(v)
-            e = gol.Engine(W, H, device=0, band_rows=b)
-            e.set_stream(stream.cuda_stream)
-            e.fill_random(3)
-            e.step(5)
-            engines[(v, e.info().band_rows)] = e
+            for k in [int(x) for x in a.tpl.split(",")]:
+                os.environ["GOL_STENCIL_VARIANT"] = str(v)
+                e = gol.Engine(W, H, device=0, band_rows=b, turns_per_launch=k)
+                e.set_stream(stream.cuda_stream)
+                e.fill_random(3)
+                e.step(5)
+                engines[(v, e.info().band_rows, k)] = e
     torch.cuda.synchronize()
     res = {k: [] for k in engines}
     for _ in range(a.rounds):
@@ -44,7 +46,7 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            e.step(a.turns)
+            e.step(a.turns)       # turns: a multiple of every tpl keeps launches uniform
             e1.record(stream)
             e1.synchronize()
             res[k].append(e0.elapsed_time(e1) * 1e3 / a.turns)
@@ -53,7 +55,7 @@ def main():
     for k, ts in res.items():
         us = statistics.median(ts)
         gbs = 0.25 * W * H / (us * 1e-6) / 1e9
-        out.append({"variant": k[0], "band": k[1], "us_per_turn": round(us, 2),
+        out.append({"variant": k[0], "band": k[1], "tpl": k[2], "us_per_turn": round(us, 2),
                     "min_us": round(min(ts), 2), "GBs": round(gbs, 1),
                     "GCUPS": round(W * H / us / 1e3, 1)})
         print(json.dumps(out[-1]), flush=True)
