@@ -47,6 +47,7 @@ struct gol_ctx {
     int band = 8;
     int variant = golk::kVariantDefault;
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
+    int multi_words = 2;                     // k_step_multi words per lane
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
     uint64_t *blocked = nullptr;
@@ -212,6 +213,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
     if (!c->fast) c->tpl = 1;
+    if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);
@@ -402,6 +404,7 @@ int gol_step(gol_ctx *c, int64_t turns)
     a.cnt_hi = own_hi(c);
     a.band = c->band;
     a.variant = c->variant;
+    a.multi_words = c->multi_words;
     for (int64_t t = 0; t < turns;) {
         // temporal blocking: fuse k turns into one pass when nothing needs per-turn output
         int k = 1;

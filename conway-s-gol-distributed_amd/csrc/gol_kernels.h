@@ -24,6 +24,7 @@ struct StepArgs {
     int cnt_lo, cnt_hi;                // rows whose outputs are counted
     int band;                          // rows per wavefront (fast) / per thread (generic)
     int variant;                       // fast-path kernel variant (kVariant*)
+    int multi_words;                   // k_step_multi words per lane (1 or 2)
 };
 
 // fast-path stencil variants (A/B-able in one process; kVariantDefault is shipped)

@@ -211,26 +211,22 @@ __global__ __launch_bounds__(256) void k_step_fast(const uint64_t *__restrict__ 
 // loads outstanding, and the loop is unrolled by Q so every slot index is a
 // compile-time constant (no register rotation moves).  xor3 / majority are single
 // v_bitop3_b32 (truth tables 0x96 / 0xE8, symmetric in their operands).
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
-{
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c)
-{
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// v_bitop3 truth-table index is (src0 << 2) | (src1 << 1) | src2 (checked against the
-// compiler's own lowering of a & ~b & ~c -> bitop3:0x10).
+// v_bitop3_b32 through the compiler builtin (no inline asm: no conservative hazard
+// s_nops, and the scheduler sees the dependencies).  Truth-table index is
+// (src0 << 2) | (src1 << 1) | src2 (checked against the compiler's own lowering of
+// a & ~b & ~c -> bitop3:0x10).
 template <int IMM>
 __device__ __forceinline__ uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c)
 {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(IMM));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return bitop3<0x96>(a, b, c);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c)
+{
+    return bitop3<0xe8>(a, b, c);
 }
 
 template <typename F, int... Is>
@@ -383,13 +379,35 @@ __global__ __launch_bounds__(256) void k_step_ring(const uint64_t *__restrict__ 
 // input rows [y0-K, y1+K) once; stage j (j = 0..K-1) turns its input row stream into
 // the stream of turn t+j+1 rows one row later, all in registers.  HBM traffic per
 // launch is one read + one write of the board for K turns: 0.25/K B per cell-update.
-constexpr int kMultiStride = kTileWords - 4;   // 124 stored words per tile
+// V = words per lane (2: 16-B accesses, 128-word tiles; 1: 8-B accesses, 64-word tiles,
+// half the per-stage registers -> higher occupancy).  Tiles store lanes 1..62.
+template <int V> struct LaneVec;
+template <> struct LaneVec<2> { using T = uint4; };
+template <> struct LaneVec<1> { using T = uint2; };
 
-template <int K>
+template <int V>
+__device__ __forceinline__ void vec_get(const typename LaneVec<V>::T &v, uint32_t (&c)[2 * V]);
+template <>
+__device__ __forceinline__ void vec_get<2>(const uint4 &v, uint32_t (&c)[4])
+{
+    c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+}
+template <>
+__device__ __forceinline__ void vec_get<1>(const uint2 &v, uint32_t (&c)[2])
+{
+    c[0] = v.x; c[1] = v.y;
+}
+__device__ __forceinline__ uint4 vec_make(const uint32_t (&c)[4]) { return make_uint4(c[0], c[1], c[2], c[3]); }
+__device__ __forceinline__ uint2 vec_make(const uint32_t (&c)[2]) { return make_uint2(c[0], c[1]); }
+
+template <int K, int V>
 __global__ __launch_bounds__(256) void k_step_multi(const uint64_t *__restrict__ in,
                                                     uint64_t *__restrict__ out, StepArgs a,
                                                     int ntx)
 {
+    constexpr int ND = 2 * V;                          // dwords per lane
+    constexpr int STRIDE = 62 * V;                     // stored words per tile
+    using Vec = typename LaneVec<V>::T;
     const int lane = threadIdx.x & 63;
     const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int tx = wv % ntx;
@@ -399,13 +417,14 @@ __global__ __launch_bounds__(256) void k_step_multi(const uint64_t *__restrict__
     const int y1 = min(y0 + a.band, a.row_hi);         // outputs [y0, y1)
 
     const int nw = a.nw;
-    const int t0 = tx * kMultiStride;                  // first stored word
-    const int t1 = min(t0 + kMultiStride, nw);         // end of stored words
-    const int last = (t1 - t0) / 2 + 1;                // right halo lane
+    const int t0 = tx * STRIDE;                        // first stored word
+    const int t1 = min(t0 + STRIDE, nw);               // end of stored words
+    const int last = (t1 - t0 + V - 1) / V + 1;        // right halo lane
     const bool act = lane <= last;
     const bool st = lane >= 1 && lane < last;
-    int w = t0 - 2 + 2 * lane;                         // lane's first word (torus wrap)
-    w = w < 0 ? w + nw : (w >= nw ? w - nw : w);
+    int w = t0 - V + V * lane;                         // lane's first word (torus wrap)
+    while (w < 0) w += nw;
+    while (w >= nw) w -= nw;
     const size_t pitch32 = (size_t)a.pitch * 2;
     const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in) + 2 * (size_t)w;
     uint32_t *out32 = reinterpret_cast<uint32_t *>(out) + 2 * (size_t)w;
@@ -415,71 +434,72 @@ __global__ __launch_bounds__(256) void k_step_multi(const uint64_t *__restrict__
         while (r >= M) r -= M;
         return (size_t)r * pitch32;
     };
-    auto load = [&](int r) -> uint4 {
-        return act ? *reinterpret_cast<const uint4 *>(in32 + rowoff(r)) : make_uint4(0, 0, 0, 0);
-    };
-    auto sums = [&](const uint4 &v, uint32_t (&s0)[4], uint32_t (&s1)[4]) {
-        const uint32_t L = dpp_from_lower(0u, v.w);
-        const uint32_t R = dpp_from_upper(0u, v.x);
-        const uint32_t c[4] = {v.x, v.y, v.z, v.w};
-        uint32_t wv_[4], e[4];
-        wv_[0] = __builtin_amdgcn_alignbit(c[0], L, 31);
-        wv_[1] = __builtin_amdgcn_alignbit(c[1], c[0], 31);
-        wv_[2] = __builtin_amdgcn_alignbit(c[2], c[1], 31);
-        wv_[3] = __builtin_amdgcn_alignbit(c[3], c[2], 31);
-        e[0] = __builtin_amdgcn_alignbit(c[1], c[0], 1);
-        e[1] = __builtin_amdgcn_alignbit(c[2], c[1], 1);
-        e[2] = __builtin_amdgcn_alignbit(c[3], c[2], 1);
-        e[3] = __builtin_amdgcn_alignbit(R, c[3], 1);
+    auto load = [&](int r, uint32_t (&c)[ND]) {
+        if (act) {
+            vec_get<V>(*reinterpret_cast<const Vec *>(in32 + rowoff(r)), c);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            s0[k] = xor3(wv_[k], c[k], e[k]);
-            s1[k] = maj(wv_[k], c[k], e[k]);
+            for (int k = 0; k < ND; ++k) c[k] = 0;
+        }
+    };
+    auto sums = [&](const uint32_t (&c)[ND], uint32_t (&s0)[ND], uint32_t (&s1)[ND]) {
+        const uint32_t L = dpp_from_lower(0u, c[ND - 1]);
+        const uint32_t R = dpp_from_upper(0u, c[0]);
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+            const uint32_t wl = __builtin_amdgcn_alignbit(c[k], k == 0 ? L : c[k - 1], 31);
+            const uint32_t er = __builtin_amdgcn_alignbit(k == ND - 1 ? R : c[k + 1], c[k], 1);
+            s0[k] = xor3(wl, c[k], er);
+            s1[k] = maj(wl, c[k], er);
         }
     };
 
     // per stage: ring of 3 row sums and 3 raw input rows (phase = step % 3)
-    uint32_t S0[K][3][4], S1[K][3][4];
-    uint4 X[K][3];
+    uint32_t S0[K][3][ND], S1[K][3][ND], X[K][3][ND];
 #pragma unroll
     for (int j = 0; j < K; ++j)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            X[j][p] = make_uint4(0, 0, 0, 0);
+        for (int p = 0; p < 3; ++p)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) S0[j][p][k] = S1[j][p][k] = 0;
-        }
-    uint4 raw[3];
+            for (int k = 0; k < ND; ++k) S0[j][p][k] = S1[j][p][k] = X[j][p][k] = 0;
+    uint32_t raw[3][ND];
     const int r_first = y0 - K, r_end = y1 + K;         // input rows [r_first, r_end)
 #pragma unroll
-    for (int p = 0; p < 3; ++p) raw[p] = (r_first + p < r_end) ? load(r_first + p) : make_uint4(0, 0, 0, 0);
+    for (int p = 0; p < 3; ++p) {
+        if (r_first + p < r_end) {
+            load(r_first + p, raw[p]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) raw[p][k] = 0;
+        }
+    }
 
     auto step = [&](auto I, int r) {                    // r = input row of this step
         constexpr int i = decltype(I)::value;
         constexpr int pn = i % 3, p1 = (i + 2) % 3, p2 = (i + 1) % 3;
-        uint4 x = raw[pn];
-        if (r + 3 < r_end) raw[pn] = load(r + 3);
+        uint32_t x[ND];
+#pragma unroll
+        for (int k = 0; k < ND; ++k) x[k] = raw[pn][k];
+        if (r + 3 < r_end) load(r + 3, raw[pn]);
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             sums(x, S0[j][pn], S1[j][pn]);
-            X[j][pn] = x;
-            const uint32_t al[4] = {X[j][p1].x, X[j][p1].y, X[j][p1].z, X[j][p1].w};
-            uint32_t o[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < ND; ++k) X[j][pn][k] = x[k];
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
                 const uint32_t u0 = xor3(S0[j][p2][k], S0[j][p1][k], S0[j][pn][k]);
                 const uint32_t u1 = maj(S0[j][p2][k], S0[j][p1][k], S0[j][pn][k]);
                 const uint32_t v0 = xor3(S1[j][p2][k], S1[j][p1][k], S1[j][pn][k]);
                 const uint32_t v1 = maj(S1[j][p2][k], S1[j][p1][k], S1[j][pn][k]);
                 const uint32_t h1 = bitop3<0x14>(u1, v0, v1);
                 const uint32_t h2 = bitop3<0x42>(u1, v0, v1);
-                const uint32_t xx = bitop3<0x08>(u0, al[k], h2);
-                o[k] = bitop3<0xea>(u0, h1, xx);
+                const uint32_t xx = bitop3<0x08>(u0, X[j][p1][k], h2);
+                x[k] = bitop3<0xea>(u0, h1, xx);         // stage j output = row r-1-j
             }
-            x = make_uint4(o[0], o[1], o[2], o[3]);     // stage j output = row r-1-j
         }
         const int ry = r - K;                            // final output row
-        if (st && ry >= y0) *reinterpret_cast<uint4 *>(out32 + rowoff(ry)) = x;
+        if (st && ry >= y0) *reinterpret_cast<Vec *>(out32 + rowoff(ry)) = vec_make(x);
     };
 
     int r = r_first;
@@ -793,17 +813,17 @@ bool multi_ok(int width, int turns)
     return fast_path_ok(width) && turns >= 2 && turns <= kMaxTurnsPerLaunch;
 }
 
-hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s)
+template <int V>
+static hipError_t launch_multi_v(const StepArgs &a, int turns, hipStream_t s)
 {
-    if (a.row_hi <= a.row_lo) return hipSuccess;
-    const int ntx = (a.nw + kMultiStride - 1) / kMultiStride;
+    const int ntx = (a.nw + 62 * V - 1) / (62 * V);
     const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
     const long long nwaves = (long long)ntx * nbands;
     const int blocks = (int)((nwaves + 3) / 4);
 #define GOL_MULTI(K)                                                                          \
     case K:                                                                                   \
-        hipLaunchKernelGGL((k_step_multi<K>), dim3(blocks), dim3(256), 0, s, a.in, a.out, a,  \
-                           ntx);                                                              \
+        hipLaunchKernelGGL((k_step_multi<K, V>), dim3(blocks), dim3(256), 0, s, a.in, a.out,  \
+                           a, ntx);                                                           \
         break;
     switch (turns) {
         GOL_MULTI(2)
@@ -817,6 +837,12 @@ hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s)
     }
 #undef GOL_MULTI
     return hipGetLastError();
+}
+
+hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s)
+{
+    if (a.row_hi <= a.row_lo) return hipSuccess;
+    return a.multi_words == 1 ? launch_multi_v<1>(a, turns, s) : launch_multi_v<2>(a, turns, s);
 }
 
 hipError_t launch_popcount(const uint64_t *w, int nw, int pitch, int row_lo, int row_hi,

@@ -131,13 +131,15 @@ def test_stencil_variants(gol, oracle, monkeypatch, variant, w, h, band):
     assert counts.tolist() == wc.astype(np.int64).tolist()
 
 
+@pytest.mark.parametrize("mw", [1, 2])
 @pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 17), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (1024, 1, 5, 8), (512, 130, 1000, 24)])
-def test_temporal_blocking(gol, oracle, tpl, w, h, band, turns):
+def test_temporal_blocking(gol, oracle, monkeypatch, mw, tpl, w, h, band, turns):
     """K turns per launch (tiles overlapping by one lane, in-register stage pipeline) is
     bit-exact for every depth, ragged tiles (8320: partial last tile), tiny tori (H < K)
-    and turn counts that leave a k=1 remainder."""
+    and turn counts that leave a k=1 remainder; 1 and 2 words per lane."""
+    monkeypatch.setenv("GOL_MULTI_WORDS", str(mw))
     with _engine(gol, w, h, band_rows=band, turns_per_launch=tpl) as e:
         assert e.info().turns_per_launch == tpl
         e.fill_random(tpl * 31 + w)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3,4")
     ap.add_argument("--bands", default="0,32,64,128")
     ap.add_argument("--tpl", default="1", help="turns per launch values")
+    ap.add_argument("--mw", default="2", help="k_step_multi words per lane values")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     W, H = a.size, a.height or a.size
@@ -33,12 +34,14 @@ def main():
     for v in [int(x) for x in a.variants.split(",")]:
         for b in [int(x) for x in a.bands.split(",")]:
             for k in [int(x) for x in a.tpl.split(",")]:
-                os.environ["GOL_STENCIL_VARIANT"] = str(v)
-                e = gol.Engine(W, H, device=0, band_rows=b, turns_per_launch=k)
-                e.set_stream(stream.cuda_stream)
-                e.fill_random(3)
-                e.step(5)
-                engines[(v, e.info().band_rows, k)] = e
+                for mw in ([int(x) for x in a.mw.split(",")] if k > 1 else [2]):
+                    os.environ["GOL_STENCIL_VARIANT"] = str(v)
+                    os.environ["GOL_MULTI_WORDS"] = str(mw)
+                    e = gol.Engine(W, H, device=0, band_rows=b, turns_per_launch=k)
+                    e.set_stream(stream.cuda_stream)
+                    e.fill_random(3)
+                    e.step(5)
+                    engines[(v, e.info().band_rows, k, mw)] = e
     torch.cuda.synchronize()
     res = {k: [] for k in engines}
     for _ in range(a.rounds):
@@ -55,7 +58,8 @@ def main():
     for k, ts in res.items():
         us = statistics.median(ts)
         gbs = 0.25 * W * H / (us * 1e-6) / 1e9
-        out.append({"variant": k[0], "band": k[1], "tpl": k[2], "us_per_turn": round(us, 2),
+        out.append({"variant": k[0], "band": k[1], "tpl": k[2], "mw": k[3],
+                    "us_per_turn": round(us, 2),
                     "min_us": round(min(ts), 2), "GBs": round(gbs, 1),
                     "GCUPS": round(W * H / us / 1e3, 1)})
         print(json.dumps(out[-1]), flush=True)
