@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Multi-rank strip rehearsal on ONE GPU: torchrun N ranks, every rank's engine on
+cuda:0, halos exchanged through gol.distributed.DistStrip over gloo (staged via host
+memory), final board gathered to rank 0 and compared with the CPU oracle.
+Used by tests/test_gpu_distributed.py; the RCCL path differs only in the backend."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "conway-s-gol-distributed_amd"), ROOT):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--height", type=int, default=1000)
+    ap.add_argument("--turns", type=int, default=53)
+    ap.add_argument("--halo", type=int, default=6)
+    ap.add_argument("--tpl", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=5)
+    a = ap.parse_args()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    import gol
+    from gol.distributed import DistStrip, EngineStrip, make_engine_strip
+    eng = make_engine_strip(a.size, a.height, rank, world, a.halo, 0, turns_per_launch=a.tpl)
+    eng.fill_random(a.seed)
+    ds = DistStrip(EngineStrip(eng, dev), rank, world, stage_on_host=True)
+    ds.step(a.turns)
+    mine = torch.from_numpy(eng.read_packed().view(np.int64))
+    parts = [torch.zeros((r, eng.words_per_row), dtype=torch.int64)
+             for _, r in gol.strip_split(a.height, world)]
+    if rank == 0:
+        dist.gather(mine, parts, dst=0)
+        got = np.concatenate([p.numpy() for p in parts]).view(np.uint64)
+        from oracle import oracle as O
+        want = O.bit_run(O.gen_random(a.seed, a.size, a.height), a.size, a.turns)
+        ok = np.array_equal(got, want)
+        print(f"dist_check world={world} halo={eng.halo} exchanges={ds.exchanges} "
+              f"tpl={a.tpl} equal={ok}", flush=True)
+        if not ok:
+            sys.exit(1)
+    else:
+        dist.gather(mine, dst=0)
+    eng.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
