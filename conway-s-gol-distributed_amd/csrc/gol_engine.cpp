@@ -35,7 +35,7 @@ namespace {
 
 constexpr int kRing = 4096;                 // per-turn count ring (turn t -> slot t % kRing)
 constexpr size_t kStagingBytes = 256u << 20;  // byte staging chunk for load / read
-constexpr int kDefaultTurnsPerLaunch = 1;     // temporal blocking off unless configured
+constexpr int kDefaultTurnsPerLaunch = 4;     // temporal blocking depth (tools/sweep.py)
 
 }  // namespace
 
@@ -48,6 +48,7 @@ struct gol_ctx {
     int variant = golk::kVariantDefault;
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
     int multi_words = 2;                     // k_step_multi words per lane
+    int band_multi = 64;                     // band height of the multi-turn kernel
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
     uint64_t *blocked = nullptr;
@@ -61,6 +62,7 @@ struct gol_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     long long turn = 0;
+    long long launches = 0;
     int halo_valid = 0;
     std::string err;
     std::recursive_mutex mu;
@@ -214,6 +216,8 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
     if (!c->fast) c->tpl = 1;
     if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
+    c->band_multi = cfg->band_rows > 0 ? cfg->band_rows
+                                       : golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);
@@ -280,6 +284,7 @@ int gol_get_info(gol_ctx *c, gol_info *info)
     info->device = c->device;
     info->turn = c->turn;
     info->nonbinary_cells = c->nonbinary;
+    info->launches = c->launches;
     return GOL_OK;
 }
 
@@ -336,6 +341,7 @@ int gol_load(gol_ctx *c, const uint8_t *bytes)
     c->nonbinary = (long long)s;
     c->cur = 0;
     c->turn = 0;
+    c->launches = 0;
     c->halo_valid = c->cfg.halo;
     c->raw_turn0.clear();
     if (s == 0) {
@@ -362,6 +368,7 @@ int gol_load_packed(gol_ctx *c, const uint64_t *words)
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
     c->turn = 0;
+    c->launches = 0;
     c->nonbinary = 0;
     c->raw_turn0.clear();
     c->halo_valid = c->cfg.halo;
@@ -380,6 +387,7 @@ int gol_fill_random(gol_ctx *c, uint64_t seed)
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
     c->turn = 0;
+    c->launches = 0;
     c->nonbinary = 0;
     c->raw_turn0.clear();
     c->halo_valid = c->cfg.halo;
@@ -429,7 +437,9 @@ int gol_step(gol_ctx *c, int64_t turns)
         if (k > 1) {
             a.blocked = nullptr;
             a.counts = nullptr;
+            a.band = c->band_multi;
             HIP_OR_FAIL(c, golk::launch_step_multi(a, k, c->stream));
+            a.band = c->band;
         } else {
             a.blocked = c->blocked_pending ? c->blocked : nullptr;
             a.counts = nullptr;
@@ -449,6 +459,7 @@ int gol_step(gol_ctx *c, int64_t turns)
         }
         c->cur ^= 1;
         c->turn += k;
+        c->launches += 1;
         t += k;
         if (is_strip(c)) c->halo_valid -= k;
         if (c->blocked_pending) {

@@ -47,6 +47,7 @@ bool fast_path_ok(int width);
 // no counts.  turns in {2, 3, 4, 5, 6, 8}.
 constexpr int kMaxTurnsPerLaunch = 8;
 bool multi_ok(int width, int turns);
+int auto_band_multi(int width, int rows, int words_per_lane);
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);

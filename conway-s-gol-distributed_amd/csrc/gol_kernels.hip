@@ -808,6 +808,18 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
     return hipGetLastError();
 }
 
+int auto_band_multi(int width, int rows, int words_per_lane)
+{
+    const int nw = (width + 63) / 64;
+    const long long ntx = (nw + 62 * words_per_lane - 1) / (62 * words_per_lane);
+    // a band re-reads 2K halo rows and runs 2K pipeline fill steps, so bands are taller
+    // than for k=1: 64 rows at 65536^2 (9216 wavefronts), 16 at 16384^2 (measured).
+    long long b = (long long)rows * ntx / 9216;
+    if (b < 16) b = 16;
+    if (b > 64) b = 64;
+    return (int)b;
+}
+
 bool multi_ok(int width, int turns)
 {
     return fast_path_ok(width) && turns >= 2 && turns <= kMaxTurnsPerLaunch;

@@ -58,7 +58,8 @@ class gol_info(ctypes.Structure):
                 ("fast_path", ctypes.c_int32), ("band_rows", ctypes.c_int32),
                 ("halo_valid", ctypes.c_int32), ("turns_per_launch", ctypes.c_int32),
                 ("device", ctypes.c_int32),
-                ("turn", ctypes.c_int64), ("nonbinary_cells", ctypes.c_int64)]
+                ("turn", ctypes.c_int64), ("nonbinary_cells", ctypes.c_int64),
+                ("launches", ctypes.c_int64)]
 
 
 class gol_params(ctypes.Structure):

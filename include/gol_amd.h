@@ -87,6 +87,7 @@ typedef struct gol_info {
     int32_t  device;
     int64_t  turn;              /* completed turns since load                          */
     int64_t  nonbinary_cells;   /* cells that were neither 0 nor 255 at load           */
+    int64_t  launches;          /* stencil kernel launches since load                  */
 } gol_info;
 
 /* Whole-board (torus) engine on the current device. */
