@@ -400,8 +400,11 @@ __device__ __forceinline__ void vec_get<1>(const uint2 &v, uint32_t (&c)[2])
 __device__ __forceinline__ uint4 vec_make(const uint32_t (&c)[4]) { return make_uint4(c[0], c[1], c[2], c[3]); }
 __device__ __forceinline__ uint2 vec_make(const uint32_t (&c)[2]) { return make_uint2(c[0], c[1]); }
 
+#ifndef MULTI_MIN_WAVES
+#define MULTI_MIN_WAVES 1   // forcing 4-5 waves/SIMD spills (measured with -Rpass-analysis)
+#endif
 template <int K, int V>
-__global__ __launch_bounds__(256) void k_step_multi(const uint64_t *__restrict__ in,
+__global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint64_t *__restrict__ in,
                                                     uint64_t *__restrict__ out, StepArgs a,
                                                     int ntx)
 {
@@ -483,9 +486,18 @@ __global__ __launch_bounds__(256) void k_step_multi(const uint64_t *__restrict__
         if (r + 3 < r_end) load(r + 3, raw[pn]);
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            sums(x, S0[j][pn], S1[j][pn]);
+            // row sums of the new input row, dword by dword, each consumed right away by
+            // the rule so the oldest row's sums die early (register pressure)
+            const uint32_t L = dpp_from_lower(0u, x[ND - 1]);
+            const uint32_t R = dpp_from_upper(0u, x[0]);
 #pragma unroll
-            for (int k = 0; k < ND; ++k) X[j][pn][k] = x[k];
+            for (int k = 0; k < ND; ++k) {
+                const uint32_t wl = __builtin_amdgcn_alignbit(x[k], k == 0 ? L : x[k - 1], 31);
+                const uint32_t er = __builtin_amdgcn_alignbit(k == ND - 1 ? R : x[k + 1], x[k], 1);
+                S0[j][pn][k] = xor3(wl, x[k], er);
+                S1[j][pn][k] = maj(wl, x[k], er);
+                X[j][pn][k] = x[k];
+            }
 #pragma unroll
             for (int k = 0; k < ND; ++k) {
                 const uint32_t u0 = xor3(S0[j][p2][k], S0[j][p1][k], S0[j][pn][k]);
@@ -500,6 +512,9 @@ __global__ __launch_bounds__(256) void k_step_multi(const uint64_t *__restrict__
         }
         const int ry = r - K;                            // final output row
         if (st && ry >= y0) *reinterpret_cast<Vec *>(out32 + rowoff(ry)) = vec_make(x);
+#ifdef GOL_MULTI_SCHED_BARRIER
+        __builtin_amdgcn_sched_barrier(0);               // keep steps from interleaving
+#endif
     };
 
     int r = r_first;
