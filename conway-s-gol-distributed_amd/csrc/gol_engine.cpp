@@ -35,7 +35,6 @@ namespace {
 
 constexpr int kRing = 4096;                 // per-turn count ring (turn t -> slot t % kRing)
 constexpr size_t kStagingBytes = 256u << 20;  // byte staging chunk for load / read
-constexpr int kDefaultTurnsPerLaunch = 4;     // temporal blocking depth (tools/sweep.py)
 
 }  // namespace
 
@@ -211,11 +210,15 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         const int k = atoi(v);
         if (k >= 0 && k < golk::kVariantCount) c->variant = k;
     }
-    c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : kDefaultTurnsPerLaunch;
+    // temporal blocking defaults (tools/sweep.py on MI355X): 1 word per lane (more waves,
+    // 87 VGPRs at K=4), K = 6 on large boards (64-row bands), K = 4 on smaller ones
+    c->multi_words = 1;
+    if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
+    const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
+    c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 6 : 4);
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
     if (!c->fast) c->tpl = 1;
-    if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
     c->band_multi = cfg->band_rows > 0 ? cfg->band_rows
                                        : golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
     c->halo_valid = cfg->halo;

@@ -445,18 +445,6 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
             for (int k = 0; k < ND; ++k) c[k] = 0;
         }
     };
-    auto sums = [&](const uint32_t (&c)[ND], uint32_t (&s0)[ND], uint32_t (&s1)[ND]) {
-        const uint32_t L = dpp_from_lower(0u, c[ND - 1]);
-        const uint32_t R = dpp_from_upper(0u, c[0]);
-#pragma unroll
-        for (int k = 0; k < ND; ++k) {
-            const uint32_t wl = __builtin_amdgcn_alignbit(c[k], k == 0 ? L : c[k - 1], 31);
-            const uint32_t er = __builtin_amdgcn_alignbit(k == ND - 1 ? R : c[k + 1], c[k], 1);
-            s0[k] = xor3(wl, c[k], er);
-            s1[k] = maj(wl, c[k], er);
-        }
-    };
-
     // per stage: ring of 3 row sums and 3 raw input rows (phase = step % 3)
     uint32_t S0[K][3][ND], S1[K][3][ND], X[K][3][ND];
 #pragma unroll
