@@ -7,8 +7,9 @@ cd /tmp && export TMPDIR=/tmp
 O="$R/gpurun_out/prof"
 mkdir -p "$O"
 STEPS=${STEPS:-200}
+# the kernel-trace pass profiles exactly the driver's default bench command
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps "$STEPS" --no-cpu-baseline > "$O/kt.log" 2>&1
+  python3 "$R/bench.py" > "$O/kt.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o run --output-format csv -- \
   python3 "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline > "$O/fetch.log" 2>&1
