@@ -465,15 +465,18 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
         }
     }
 
-    auto step = [&](auto I, int r) {                    // r = input row of this step
+    // One pipeline step: input row r enters stage 0, every active stage advances one row.
+    // I = ring phase (step % 3), NS = active stages (compile-time).
+    auto step = [&](auto I, auto NSc, int r) {
         constexpr int i = decltype(I)::value;
+        constexpr int NS = decltype(NSc)::value;
         constexpr int pn = i % 3, p1 = (i + 2) % 3, p2 = (i + 1) % 3;
         uint32_t x[ND];
 #pragma unroll
         for (int k = 0; k < ND; ++k) x[k] = raw[pn][k];
         if (r + 3 < r_end) load(r + 3, raw[pn]);
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
+        for (int j = 0; j < NS; ++j) {
             // row sums of the new input row, dword by dword, each consumed right away by
             // the rule so the oldest row's sums die early (register pressure)
             const uint32_t L = dpp_from_lower(0u, x[ND - 1]);
@@ -498,21 +501,31 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
                 x[k] = bitop3<0xea>(u0, h1, xx);         // stage j output = row r-1-j
             }
         }
-        const int ry = r - K;                            // final output row
-        if (st && ry >= y0) *reinterpret_cast<Vec *>(out32 + rowoff(ry)) = vec_make(x);
-#ifdef GOL_MULTI_SCHED_BARRIER
-        __builtin_amdgcn_sched_barrier(0);               // keep steps from interleaving
-#endif
+        if constexpr (NS == K) {
+            const int ry = r - K;                        // final output row
+            if (st && ry >= y0) *reinterpret_cast<Vec *>(out32 + rowoff(ry)) = vec_make(x);
+        }
     };
 
+    // Prologue: stage j's first needed output (row y0-K+1+j) comes at step 2j+2 and its
+    // window fills in the two steps before, so step s runs stages 0 .. s/2 only.  The
+    // band always has >= 2K steps, so the prologue (2K-2 steps) never overruns it.
     int r = r_first;
+    unroll_seq(std::make_integer_sequence<int, 2 * K - 2>{}, [&](auto S) {
+        constexpr int sidx = decltype(S)::value;
+        step(std::integral_constant<int, sidx % 3>{}, std::integral_constant<int, sidx / 2 + 1>{},
+             r + sidx);
+    });
+    r += 2 * K - 2;
+    constexpr int P0 = (2 * K - 2) % 3;                 // ring phase of the first steady step
+    using Kc = std::integral_constant<int, K>;
     for (; r + 3 <= r_end; r += 3) {
-        step(std::integral_constant<int, 0>{}, r);
-        step(std::integral_constant<int, 1>{}, r + 1);
-        step(std::integral_constant<int, 2>{}, r + 2);
+        step(std::integral_constant<int, P0>{}, Kc{}, r);
+        step(std::integral_constant<int, (P0 + 1) % 3>{}, Kc{}, r + 1);
+        step(std::integral_constant<int, (P0 + 2) % 3>{}, Kc{}, r + 2);
     }
-    if (r < r_end) step(std::integral_constant<int, 0>{}, r);
-    if (r + 1 < r_end) step(std::integral_constant<int, 1>{}, r + 1);
+    if (r < r_end) step(std::integral_constant<int, P0>{}, Kc{}, r);
+    if (r + 1 < r_end) step(std::integral_constant<int, (P0 + 1) % 3>{}, Kc{}, r + 1);
 }
 
 // ---------------------------------------------------- K1g: generic stencil
