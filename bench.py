@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=65536, help="board side (default 65536)")
     ap.add_argument("--seed", type=int, default=3)
-    ap.add_argument("--halo", type=int, default=64,
+    ap.add_argument("--halo", type=int, default=128,
                     help="strip halo depth (rows exchanged every `halo` turns, N > 1)")
     ap.add_argument("--band", type=int, default=0, help="stencil band rows (0 = auto)")
     ap.add_argument("--tpl", type=int, default=0,

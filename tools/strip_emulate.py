@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Per-rank cost of the N-GPU strip path, measured on ONE GPU: rank 0's strip
+(H/N rows + halo) of the W x H board, stepped exactly as DistStrip steps it, with the
+halo exchange replaced by local device copies (export -> import of the strip's own
+boundary rows, i.e. the N=1 torus of that strip: same bytes moved on-device, no RCCL).
+Prints per-turn time and the implied aggregate GCUPS at N GPUs (an upper bound: the
+RCCL transfer itself is not included)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "conway-s-gol-distributed_amd"))
+import torch  # noqa: E402
+
+import gol  # noqa: E402
+from gol.distributed import EngineStrip, make_engine_strip  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=65536)
+    ap.add_argument("--n", default="2,4,8")
+    ap.add_argument("--halo", default="64,128,256")
+    ap.add_argument("--turns", type=int, default=768)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for n in [int(x) for x in a.n.split(",")]:
+        for halo in [int(x) for x in a.halo.split(",")]:
+            eng = make_engine_strip(a.size, a.size, 0, n, halo, 0)
+            es = EngineStrip(eng, dev)
+            eng.fill_random(3)
+            with torch.cuda.stream(es.stream):
+                def run(turns):
+                    left = turns
+                    while left:
+                        if es.halo_valid == 0:
+                            top, bot = es.export_rows()
+                            es.import_rows(bot, top)        # local stand-in for the exchange
+                        m = min(left, es.halo_valid)
+                        es.step(m)
+                        left -= m
+                run(2 * halo)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(es.stream)
+                run(a.turns)
+                e1.record(es.stream)
+                e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.turns
+            info = eng.info()
+            print(json.dumps({"n": n, "halo": info.halo, "rows": info.rows,
+                              "tpl": info.turns_per_launch, "us_per_turn": round(us, 2),
+                              "aggregate_GCUPS_upper": round(a.size * a.size / us / 1e3, 1)}),
+                  flush=True)
+            eng.close()
+
+
+if __name__ == "__main__":
+    main()
