@@ -219,11 +219,18 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
     if (!c->fast) c->tpl = 1;
-    c->band_multi = cfg->band_rows > 0 ? cfg->band_rows
-                                       : golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);
+    c->band_multi = cfg->band_rows;
+    if (c->band_multi <= 0 && c->tpl > 1) {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int bpc = golk::multi_blocks_per_cu(c->tpl, c->multi_words);
+        c->band_multi = golk::pick_band_multi(cfg->width, cfg->rows, c->multi_words, c->tpl,
+                                              ncu * bpc * 4);
+    }
+    if (c->band_multi <= 0) c->band_multi = golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
     const size_t words = (size_t)c->buf_rows * c->pitch;
     int rc = GOL_OK;
     auto bail = [&](int code) {

@@ -48,6 +48,10 @@ bool fast_path_ok(int width);
 constexpr int kMaxTurnsPerLaunch = 8;
 bool multi_ok(int width, int turns);
 int auto_band_multi(int width, int rows, int words_per_lane);
+// resident 256-thread blocks per CU of k_step_multi<turns, words_per_lane> (0 on error)
+int multi_blocks_per_cu(int turns, int words_per_lane);
+// band height minimising (residency rounds x per-wavefront work) for the multi kernel
+int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capacity_waves);
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);

@@ -867,6 +867,61 @@ static hipError_t launch_multi_v(const StepArgs &a, int turns, hipStream_t s)
     return hipGetLastError();
 }
 
+template <int V>
+static int multi_blocks_per_cu_v(int turns)
+{
+    int blocks = 0;
+    hipError_t e = hipErrorInvalidValue;
+#define GOL_OCC(K)                                                                            \
+    case K:                                                                                   \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_step_multi<K, V>, 256, 0); \
+        break;
+    switch (turns) {
+        GOL_OCC(2)
+        GOL_OCC(3)
+        GOL_OCC(4)
+        GOL_OCC(5)
+        GOL_OCC(6)
+        GOL_OCC(8)
+    default:
+        break;
+    }
+#undef GOL_OCC
+    return e == hipSuccess ? blocks : 0;
+}
+
+int multi_blocks_per_cu(int turns, int words_per_lane)
+{
+    return words_per_lane == 1 ? multi_blocks_per_cu_v<1>(turns) : multi_blocks_per_cu_v<2>(turns);
+}
+
+int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capacity_waves)
+{
+    // Every wavefront of a launch does the same work, so a launch takes ~ rounds x
+    // (per-wavefront time), rounds = ceil(waves / resident capacity): a grid that spills
+    // a few waves into an extra round wastes most of that round (measured: the 65536^2
+    // K=6 launch at 4.25 rounds).  Per-wavefront time ~ K x band + K (K + 1) stage-steps
+    // (band rows, 2K halo rows, minus the skipped pipeline fill).  Pick the band that
+    // minimises rounds x per-wave time; ties go to the smaller band.
+    const int nw = (width + 63) / 64;
+    const long long ntx = (nw + 62 * words_per_lane - 1) / (62 * words_per_lane);
+    if (capacity_waves <= 0) return auto_band_multi(width, rows, words_per_lane);
+    long long best_cost = -1;
+    int best = 16;
+    for (int band = 16; band <= 1024; ++band) {
+        const long long nb = (rows + band - 1) / band;
+        const long long waves = ntx * nb;
+        const long long rounds = (waves + capacity_waves - 1) / capacity_waves;
+        const long long cost = rounds * ((long long)turns * band + (long long)turns * (turns + 1));
+        if (best_cost < 0 || cost < best_cost) {
+            best_cost = cost;
+            best = band;
+        }
+        if (nb == 1) break;
+    }
+    return best;
+}
+
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s)
 {
     if (a.row_hi <= a.row_lo) return hipSuccess;

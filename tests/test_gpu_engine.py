@@ -96,10 +96,11 @@ RANDOM_CASES = [
 ]
 
 
+@pytest.mark.parametrize("tpl", [1, 0])
 @pytest.mark.parametrize("w,h,turns", RANDOM_CASES)
-def test_random_vs_oracle(gol, oracle, w, h, turns):
+def test_random_vs_oracle(gol, oracle, w, h, turns, tpl):
     seed = w * 7919 + h
-    with _engine(gol, w, h) as e:
+    with _engine(gol, w, h, turns_per_launch=tpl) as e:
         e.fill_random(seed)
         start = e.read_packed()
         assert np.array_equal(start, oracle.gen_random(seed, w, h))
@@ -219,9 +220,10 @@ def test_nonbinary_cells(gol, oracle, w, h):
 
 
 # ------------------------------------------------------- strips in-process
+@pytest.mark.parametrize("tpl", [1, 0])
 @pytest.mark.parametrize("n,K", [(1, 1), (2, 1), (2, 4), (3, 2), (4, 16), (7, 3), (8, 5)])
 @pytest.mark.parametrize("w", [512, 100])
-def test_strips_in_process(gol, oracle, n, K, w):
+def test_strips_in_process(gol, oracle, n, K, w, tpl):
     """Row strips with K-row halos exchanged every K turns == torus, for any N (the
     reference's results are independent of len(SUB): Server/gol/distributor.go:106-116)."""
     h, turns, seed = 120, 23, 4
@@ -229,7 +231,8 @@ def test_strips_in_process(gol, oracle, n, K, w):
     want = oracle.ref_run(board, turns, nsub=max(1, n), threads=2)
     parts = gol.strip_split(h, n)
     Kp = min(K, min(r for _, r in parts))
-    engs = [gol.Engine(w, h, device=0, row_offset=o, rows=r, halo=Kp) for o, r in parts]
+    engs = [gol.Engine(w, h, device=0, row_offset=o, rows=r, halo=Kp, turns_per_launch=tpl)
+            for o, r in parts]
     try:
         for e, (o, r) in zip(engs, parts):
             e.load(gol.haloed_rows(board, o, r, Kp))

@@ -54,4 +54,9 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception:
+        import traceback
+        print(f"RANK {os.environ.get('RANK')} FAILED:\n" + traceback.format_exc(), flush=True)
+        raise
