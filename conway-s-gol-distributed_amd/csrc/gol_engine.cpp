@@ -288,7 +288,7 @@ int gol_get_info(gol_ctx *c, gol_info *info)
     info->pitch_words = c->pitch;
     info->buffer_rows = c->buf_rows;
     info->fast_path = c->fast ? 1 : 0;
-    info->band_rows = c->band;
+    info->band_rows = c->tpl > 1 ? c->band_multi : c->band;   // band of the kernel in use
     info->halo_valid = c->halo_valid;
     info->turns_per_launch = c->tpl;
     info->device = c->device;

@@ -902,7 +902,9 @@ int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capa
     // a few waves into an extra round wastes most of that round (measured: the 65536^2
     // K=6 launch at 4.25 rounds).  Per-wavefront time ~ K x band + K (K + 1) stage-steps
     // (band rows, 2K halo rows, minus the skipped pipeline fill).  Pick the band that
-    // minimises rounds x per-wave time; ties go to the smaller band.
+    // minimises rounds x per-wave time, charging at least 2 rounds (a single round that
+    // starts and ends every wavefront together measured slower: 65536^2 K=6 band 274 vs
+    // 137, 60.6 vs 58.0 us/turn); ties go to the smaller band.
     const int nw = (width + 63) / 64;
     const long long ntx = (nw + 62 * words_per_lane - 1) / (62 * words_per_lane);
     if (capacity_waves <= 0) return auto_band_multi(width, rows, words_per_lane);
@@ -911,7 +913,8 @@ int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capa
     for (int band = 16; band <= 1024; ++band) {
         const long long nb = (rows + band - 1) / band;
         const long long waves = ntx * nb;
-        const long long rounds = (waves + capacity_waves - 1) / capacity_waves;
+        long long rounds = (waves + capacity_waves - 1) / capacity_waves;
+        if (rounds < 2) rounds = 2;
         const long long cost = rounds * ((long long)turns * band + (long long)turns * (turns + 1));
         if (best_cost < 0 || cost < best_cost) {
             best_cost = cost;

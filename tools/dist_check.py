@@ -34,12 +34,14 @@ def main():
     eng.fill_random(a.seed)
     ds = DistStrip(EngineStrip(eng, dev), rank, world, stage_on_host=True)
     ds.step(a.turns)
-    mine = torch.from_numpy(eng.read_packed().view(np.int64))
-    parts = [torch.zeros((r, eng.words_per_row), dtype=torch.int64)
-             for _, r in gol.strip_split(a.height, world)]
+    split = gol.strip_split(a.height, world)
+    maxr = max(r for _, r in split)
+    mine = torch.zeros((maxr, eng.words_per_row), dtype=torch.int64)   # gloo gather: equal sizes
+    mine[: eng.rows] = torch.from_numpy(eng.read_packed().view(np.int64))
+    parts = [torch.zeros((maxr, eng.words_per_row), dtype=torch.int64) for _ in split]
     if rank == 0:
         dist.gather(mine, parts, dst=0)
-        got = np.concatenate([p.numpy() for p in parts]).view(np.uint64)
+        got = np.concatenate([p.numpy()[:r] for p, (_, r) in zip(parts, split)]).view(np.uint64)
         from oracle import oracle as O
         want = O.bit_run(O.gen_random(a.seed, a.size, a.height), a.size, a.turns)
         ok = np.array_equal(got, want)

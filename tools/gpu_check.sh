@@ -25,9 +25,10 @@ for step in "$@"; do
     pmcsq)  run pmcsq 300 bash tools/pmc_sq.sh ;;
     pmcsq1) run pmcsq1 300 env TAG=_k1 BENCH_ARGS="--tpl 1" bash tools/pmc_sq.sh ;;
     strips) run strips 300 python -u tools/strip_emulate.py ;;
+    stripsk) run stripsk 400 python -u tools/strip_emulate.py --halo 120 --tpl 4,6,8 ;;
     dist)   run t_dist 400 python -u -m pytest tests/test_gpu_distributed.py -v --timeout 300 --timeout-method thread ;;
     tbq)    run tbq 500 python -u tools/sweep.py --variants 2 --bands 0,64,128,137,200,240,274,300,400 --tpl 6,8 --mw 1 --turns 120 ;;
-    tbq16k) run tbq16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 0,16,20,24,32,48 --tpl 4,6 --mw 1 --turns 960 ;;
+    tbq16k) run tbq16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 0,16,20,24,32,48 --tpl 4,6,8 --mw 1 --turns 960 ;;
     sweep)  run sweep 400 python -u tools/sweep.py --variants 2,4,5,6 --bands 16,32,64,128,256 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac

@@ -24,11 +24,12 @@ def main():
     ap.add_argument("--n", default="2,4,8")
     ap.add_argument("--halo", default="64,128,256")
     ap.add_argument("--turns", type=int, default=768)
+    ap.add_argument("--tpl", default="0")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for n in [int(x) for x in a.n.split(",")]:
-        for halo in [int(x) for x in a.halo.split(",")]:
-            eng = make_engine_strip(a.size, a.size, 0, n, halo, 0)
+        for halo, tpl in [(int(h), int(t)) for h in a.halo.split(",") for t in a.tpl.split(",")]:
+            eng = make_engine_strip(a.size, a.size, 0, n, halo, 0, turns_per_launch=tpl)
             es = EngineStrip(eng, dev)
             eng.fill_random(3)
             with torch.cuda.stream(es.stream):
@@ -49,7 +50,7 @@ def main():
                 e1.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.turns
             info = eng.info()
-            print(json.dumps({"n": n, "halo": info.halo, "rows": info.rows,
+            print(json.dumps({"n": n, "halo": info.halo, "rows": info.rows, "band": info.band_rows,
                               "tpl": info.turns_per_launch, "us_per_turn": round(us, 2),
                               "aggregate_GCUPS_upper": round(a.size * a.size / us / 1e3, 1)}),
                   flush=True)
