@@ -38,6 +38,22 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+// The reference Server keeps `world` and `turn` in process globals across controller
+// runs (Server/gol/distributor.go:29-30) so that CONT=yes can resume
+// (Local/gol/distributor.go:171-178).  Here: the last run's final packed board.
+struct RetainedState {
+    std::mutex mu;
+    bool valid = false;
+    int W = 0, H = 0;
+    long long turn = 0;
+    std::vector<uint64_t> words;     // H x ceil(W/64)
+};
+RetainedState &retained()
+{
+    static RetainedState r;
+    return r;
+}
+
 struct Item {
     gol_event ev;
     std::shared_ptr<std::vector<int64_t>> cells;   // FinalTurnComplete.Alive
@@ -97,6 +113,7 @@ struct gol_run {
     int ngpus = 1;
     std::vector<int> devices;
     int halo = 0;
+    int resume = -1;
     int ticker_ms = 2000;
     size_t capacity = 1;
     bool emit_turn_complete = false;
@@ -232,6 +249,42 @@ struct Strips {
         return GOL_OK;
     }
 
+    int nwords() const { return (W + 63) / 64; }
+
+    // load a global packed board (H x nw words) into every strip (with halo rows)
+    int load_packed(const std::vector<uint64_t> &g)
+    {
+        const size_t nw = (size_t)nwords();
+        if (!strip_mode()) {
+            int rc = gol_load_packed(eng[0], g.data());
+            return rc ? fail_from(eng[0], rc) : GOL_OK;
+        }
+        for (size_t i = 0; i < eng.size(); i++) {
+            const int br = rows[i] + 2 * K;
+            std::vector<uint64_t> buf((size_t)br * nw);
+            for (int b = 0; b < br; b++) {
+                int gr = (off[i] - K + b) % H;
+                if (gr < 0) gr += H;
+                std::memcpy(buf.data() + (size_t)b * nw, g.data() + (size_t)gr * nw, nw * 8);
+            }
+            int rc = gol_load_packed(eng[i], buf.data());
+            if (rc) return fail_from(eng[i], rc);
+        }
+        return GOL_OK;
+    }
+
+    int read_packed(std::vector<uint64_t> &g)
+    {
+        const size_t nw = (size_t)nwords();
+        g.assign((size_t)H * nw, 0);
+        for (size_t i = 0; i < eng.size(); i++) {
+            const int o = strip_mode() ? off[i] : 0;
+            int rc = gol_read_packed(eng[i], g.data() + (size_t)o * nw);
+            if (rc) return fail_from(eng[i], rc);
+        }
+        return GOL_OK;
+    }
+
     int halo_valid()
     {
         gol_info info;
@@ -362,6 +415,21 @@ void gol_run::run()
     if (st.load(pix)) return die(st.err);
 
     long long turn = 0;
+    bool cont = resume > 0;
+    if (resume < 0) {
+        const char *e = getenv("CONT");                // distributor.go:171
+        cont = e && std::string(e) == "yes";
+    }
+    if (cont) {
+        // GetWorld -> {SWorld, TurnCur}; run Turns - TurnCur more turns (distributor.go:172-177)
+        RetainedState &rs = retained();
+        std::lock_guard<std::mutex> lk(rs.mu);
+        if (!rs.valid || rs.W != W || rs.H != H)
+            return die("CONT=yes: no retained board of this size to resume from");
+        if (st.load_packed(rs.words)) return die(st.err);
+        turn = rs.turn;
+    }
+    const long long turn0 = turn;   // engines count from 0; events report turn0 + engine turn
     gol_event ev = make_ev(GOL_EV_STATE_CHANGE, turn);
     ev.new_state = GOL_EXECUTING;
     if (!send(ev)) return close();
@@ -384,7 +452,7 @@ void gol_run::run()
         next_tick += std::chrono::milliseconds(ticker_ms);
         long long t = 0, a = 0;
         if (st.snapshot(t, a)) { die(st.err); return false; }
-        gol_event e = make_ev(GOL_EV_ALIVE_CELLS_COUNT, t);
+        gol_event e = make_ev(GOL_EV_ALIVE_CELLS_COUNT, turn0 + t);
         e.cells_count = a;
         return send(e);
     };
@@ -405,7 +473,7 @@ void gol_run::run()
     pix.shrink_to_fit();
 
     long long chunk = 1;
-    bool quit = false;
+    bool quit = false, killed = false;
     while (turn < p.turns && !quit) {
         if (abort.load()) return close();
         int k;
@@ -414,6 +482,7 @@ void gol_run::run()
                 if (!save_image(turn)) return close();
             } else if (k == 'q' || k == 'k') {        // :113-115, :146-150
                 quit = true;
+                killed = killed || k == 'k';
             } else if (k == 'p') {                    // :117-130, Server :147-156
                 gol_event e = make_ev(GOL_EV_STATE_CHANGE, turn);
                 e.new_state = GOL_PAUSED;
@@ -466,6 +535,22 @@ void gol_run::run()
         }
     }
 
+    // retain the final board for a later CONT=yes run; 'k' kills the "server" and its state
+    {
+        RetainedState &rs = retained();
+        std::lock_guard<std::mutex> lk(rs.mu);
+        rs.valid = false;
+        if (!killed) {
+            if (st.read_packed(rs.words)) return die(st.err);
+            rs.W = W;
+            rs.H = H;
+            rs.turn = turn;
+            rs.valid = true;
+        } else {
+            rs.words.clear();
+        }
+    }
+
     // FinalTurnComplete{turn, calculateAliveCells} -> StateChange Quitting ->
     // PGM out/WxHxT -> ImageOutputComplete -> close  (distributor.go:187-226)
     auto cells = std::make_shared<std::vector<int64_t>>();
@@ -502,6 +587,7 @@ int gol_run_start(const gol_params *p, const gol_run_options *o, gol_run **out)
         r->emit_turn_complete = o->emit_turn_complete != 0;
         r->emit_cell_flipped = o->emit_cell_flipped != 0;
         r->engine_flags = o->engine_flags;
+        r->resume = o->resume;
     }
     for (int i = 0; i < r->ngpus; i++)
         r->devices.push_back(o && o->devices ? o->devices[i] : i % ndev);

@@ -208,7 +208,7 @@ def Run(p: Params, events: Channel, keyPresses: Optional[Channel] = None, *,
         devices: Optional[list] = None, halo: int = 0, ticker_ms: int = 2000,
         event_capacity: int = 1, emit_turn_complete: bool = True,
         emit_cell_flipped: bool = False, count_every_turn: bool = False,
-        alive_as_array: bool = False) -> RunHandle:
+        alive_as_array: bool = False, resume: Optional[bool] = None) -> RunHandle:
     """Start a run and return immediately (reference ``gol.Run``, Local/gol/gol.go:12-40).
 
     Events arrive on ``events`` in the reference's order
@@ -216,7 +216,8 @@ def Run(p: Params, events: Channel, keyPresses: Optional[Channel] = None, *,
     [TurnComplete{t} per turn], AliveCellsCount every ``ticker_ms``,
     FinalTurnComplete, StateChange{T, Quitting}, ImageOutputComplete{T, "WxHxT"},
     then the channel is closed.  ``ngpus`` = number of row strips (the
-    reference's ``len(SUB)``), one engine each.
+    reference's ``len(SUB)``), one engine each.  ``resume`` = the reference's
+    ``CONT=yes`` (None: read the CONT environment variable).
     """
     L = N.lib()
     prm = N.gol_params(int(p.Turns), int(p.Threads), int(p.ImageWidth), int(p.ImageHeight))
@@ -234,6 +235,7 @@ def Run(p: Params, events: Channel, keyPresses: Optional[Channel] = None, *,
     opts.emit_turn_complete = 1 if emit_turn_complete else 0
     opts.emit_cell_flipped = 1 if emit_cell_flipped else 0
     opts.engine_flags = N.GOL_FLAG_COUNT_EVERY_TURN if count_every_turn else 0
+    opts.resume = -1 if resume is None else (1 if resume else 0)
     h = ctypes.c_void_p()
     N.check(L.gol_run_start(ctypes.byref(prm), ctypes.byref(opts), ctypes.byref(h)))
     handle = RunHandle(h, L)

@@ -79,7 +79,8 @@ class gol_run_options(ctypes.Structure):
                 ("ngpus", ctypes.c_int32), ("devices", ctypes.POINTER(ctypes.c_int32)),
                 ("halo", ctypes.c_int32), ("ticker_ms", ctypes.c_int32),
                 ("event_capacity", ctypes.c_int32), ("emit_turn_complete", ctypes.c_int32),
-                ("emit_cell_flipped", ctypes.c_int32), ("engine_flags", ctypes.c_uint32)]
+                ("emit_cell_flipped", ctypes.c_int32), ("engine_flags", ctypes.c_uint32),
+                ("resume", ctypes.c_int32)]
 
 
 _lib = None

@@ -191,6 +191,11 @@ typedef struct gol_run_options {
     int32_t emit_turn_complete;      /* 1 = TurnComplete{t} for every turn (event.go:55-60) */
     int32_t emit_cell_flipped;       /* 1 = CellFlipped for initial cells and each flip  */
     uint32_t engine_flags;           /* GOL_FLAG_* for the engines                      */
+    int32_t resume;                  /* 1 = CONT=yes (Local/gol/distributor.go:171-178): continue
+                                        from the board and turn the previous run in this
+                                        process ended with (the reference Server's retained
+                                        world/turn), running Turns - turn more turns; -1 =
+                                        read the CONT environment variable                 */
 } gol_run_options;
 
 typedef struct gol_run gol_run;

@@ -183,3 +183,34 @@ def test_missing_image_reports_error(gol, workdir):
     assert list(events) == []
     h.wait(5)
     assert h.error and "32x32" in h.error
+
+
+def test_cont_resume(gol, workdir, oracle):
+    """CONT=yes (Local/gol/distributor.go:171-178): a run resumes from the board and turn
+    the previous run ended with and runs Turns - TurnCur more turns; 'k' drops that state."""
+    p = gol.Params(Turns=40, Threads=4, ImageWidth=64, ImageHeight=64)
+    run_collect(gol, p, workdir, resume=False)
+    p2 = gol.Params(Turns=100, Threads=4, ImageWidth=64, ImageHeight=64)
+    evs = run_collect(gol, p2, workdir, resume=True)
+    assert evs[0].CompletedTurns == 40 and evs[0].NewState == gol.State.Executing
+    tc = [e.CompletedTurns for e in evs if isinstance(e, gol.TurnComplete)]
+    assert tc == list(range(41, 101))
+    final = [e for e in evs if isinstance(e, gol.FinalTurnComplete)][0]
+    assert final.CompletedTurns == 100
+    assert set((c.X, c.Y) for c in final.Alive) == read_alive_cells_bytes(
+        G.check_pgm_bytes(64, 100))
+    assert (workdir / "out" / "64x64x100.pgm").read_bytes() == G.check_pgm_bytes(64, 100)
+    # a killed run leaves nothing to resume
+    events, keys = gol.Channel(), gol.Channel(4)
+    h = gol.Run(gol.Params(Turns=10 ** 8, Threads=1, ImageWidth=64, ImageHeight=64), events,
+                keys, image_dir=str(workdir / "images"), out_dir=str(workdir / "out"),
+                resume=False, emit_turn_complete=False)
+    keys.send("k")
+    list(events)
+    h.wait(5)
+    events = gol.Channel()
+    h = gol.Run(p2, events, None, image_dir=str(workdir / "images"),
+                out_dir=str(workdir / "out"), resume=True)
+    assert list(events) == []
+    h.wait(5)
+    assert h.error and "CONT" in h.error
