@@ -25,11 +25,14 @@ def main():
     ap.add_argument("--halo", default="64,128,256")
     ap.add_argument("--turns", type=int, default=768)
     ap.add_argument("--tpl", default="0")
+    ap.add_argument("--band", default="0")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for n in [int(x) for x in a.n.split(",")]:
-        for halo, tpl in [(int(h), int(t)) for h in a.halo.split(",") for t in a.tpl.split(",")]:
-            eng = make_engine_strip(a.size, a.size, 0, n, halo, 0, turns_per_launch=tpl)
+        for halo, tpl, band in [(int(h), int(t), int(b)) for h in a.halo.split(",")
+                                for t in a.tpl.split(",") for b in a.band.split(",")]:
+            eng = make_engine_strip(a.size, a.size, 0, n, halo, 0, turns_per_launch=tpl,
+                                    band_rows=band)
             es = EngineStrip(eng, dev)
             eng.fill_random(3)
             with torch.cuda.stream(es.stream):
