@@ -48,6 +48,7 @@ struct gol_ctx {
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
     int multi_words = 2;                     // k_step_multi words per lane
     int band_multi = 64;                     // band height of the multi-turn kernel
+    float tuned_us_per_turn = 0.f;           // autotune's best measurement (0 = not tuned)
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
     uint64_t *blocked = nullptr;
@@ -144,6 +145,73 @@ int count_now(gol_ctx *c, long long *alive)
     return GOL_OK;
 }
 
+// Create-time timing sweep of the multi-turn kernel's (turns per launch, band) on the
+// engine's own buffers.  The fastest band depends on grid/residency quantisation and on
+// whether the two boards fit the 256 MiB MALL (tools/sweep.py, tools/strip_emulate.py:
+// 65536^2 -> band 137, 8192-row strips -> 48, 16384^2 -> 20), which no closed form
+// captured, so large engines measure.  Every candidate computes the same bits.
+void autotune_multi(gol_ctx *c, bool tune_k)
+{
+    const long long words = (long long)c->buf_rows * c->pitch;
+    if (words < (1ll << 20)) return;                 // < 64 Mi cells: keep the defaults
+    static const int kKs[] = {6, 8};
+    static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
+    golk::StepArgs a{};
+    a.width = c->cfg.width;
+    a.nw = c->nw;
+    a.pitch = c->pitch;
+    a.modrows = c->buf_rows;
+    a.row_lo = 0;
+    a.row_hi = c->buf_rows;
+    a.cnt_lo = 0;
+    a.cnt_hi = 0;
+    a.variant = c->variant;
+    a.multi_words = c->multi_words;
+    if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
+                                 c->buf_rows, 12345, c->stream) != hipSuccess)
+        return;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return;
+    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
+    float best = 0.f;
+    int best_k = c->tpl, best_b = c->band_multi;
+    std::vector<int> ks;
+    if (tune_k) ks.assign(std::begin(kKs), std::end(kKs));
+    else ks.push_back(c->tpl);
+    for (int K : ks) {
+        if (!golk::multi_ok(c->cfg.width, K)) continue;
+        for (int band : kBands) {
+            if (band > c->cfg.rows && band != kBands[0]) break;
+            a.band = band;
+            a.in = c->board[0];
+            a.out = c->board[1];
+            bool ok = golk::launch_step_multi(a, K, c->stream) == hipSuccess;   // warm
+            ok = ok && hipEventRecord(e0, c->stream) == hipSuccess;
+            for (int rep = 0; rep < 2 && ok; ++rep) {
+                a.in = c->board[(rep + 1) & 1];
+                a.out = c->board[rep & 1];
+                ok = golk::launch_step_multi(a, K, c->stream) == hipSuccess;
+            }
+            ok = ok && hipEventRecord(e1, c->stream) == hipSuccess &&
+                 hipEventSynchronize(e1) == hipSuccess;
+            float ms = 0.f;
+            if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
+            const float per_turn = ms / (2.f * K);
+            if (best == 0.f || per_turn < best) {
+                best = per_turn;
+                best_k = K;
+                best_b = band;
+            }
+        }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipGetLastError();
+    c->tpl = best_k;
+    c->band_multi = best_b;
+    c->tuned_us_per_turn = best * 1000.f;
+}
+
 }  // namespace
 
 // ================================================================ C ABI
@@ -215,7 +283,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     c->multi_words = 1;
     if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
     const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
-    c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 6 : 4);
+    c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 8 : 6);
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
     if (!c->fast) c->tpl = 1;
@@ -247,6 +315,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         return bail(rc);
     }
     c->stream = c->own_stream;
+    if (c->tpl > 1 && cfg->band_rows <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {
+        const char *at = getenv("GOL_AUTOTUNE");
+        if (!at || atoi(at) != 0) autotune_multi(c, cfg->turns_per_launch <= 0);
+    }
     if ((e = hipMemsetAsync(c->board[0], 0, words * 8, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->board[1], 0, words * 8, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->counts, 0, (size_t)(kRing + 1) * kShards * 8, c->stream)) !=

@@ -27,6 +27,7 @@ GOL_ETIMEDOUT = -8
 
 GOL_FLAG_COUNT_EVERY_TURN = 0x1
 GOL_FLAG_FORCE_GENERIC = 0x2
+GOL_FLAG_NO_AUTOTUNE = 0x4
 
 GOL_EV_ALIVE_CELLS_COUNT = 1
 GOL_EV_IMAGE_OUTPUT_COMPLETE = 2

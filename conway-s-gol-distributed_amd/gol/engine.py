@@ -18,7 +18,8 @@ from . import _native as N
 class Engine:
     def __init__(self, width: int, height: int, *, device: int = -1, row_offset: int = 0,
                  rows: int | None = None, halo: int = 0, count_every_turn: bool = False,
-                 force_generic: bool = False, band_rows: int = 0, turns_per_launch: int = 0):
+                 force_generic: bool = False, band_rows: int = 0, turns_per_launch: int = 0,
+                 autotune: bool = True):
         L = N.lib()
         cfg = N.gol_config()
         cfg.width, cfg.height = int(width), int(height)
@@ -27,7 +28,8 @@ class Engine:
         cfg.rows = int(height if rows is None else rows)
         cfg.halo = int(halo)
         cfg.flags = ((N.GOL_FLAG_COUNT_EVERY_TURN if count_every_turn else 0) |
-                     (N.GOL_FLAG_FORCE_GENERIC if force_generic else 0))
+                     (N.GOL_FLAG_FORCE_GENERIC if force_generic else 0) |
+                     (0 if autotune else N.GOL_FLAG_NO_AUTOTUNE))
         cfg.band_rows = int(band_rows)
         cfg.turns_per_launch = int(turns_per_launch)
         h = ctypes.c_void_p()

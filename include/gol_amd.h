@@ -61,6 +61,8 @@ typedef struct gol_ctx gol_ctx;
 /* flags */
 #define GOL_FLAG_COUNT_EVERY_TURN  0x1u  /* fuse a popcount into every turn (per-turn series) */
 #define GOL_FLAG_FORCE_GENERIC     0x2u  /* use the generic stencil even when the fast one applies */
+#define GOL_FLAG_NO_AUTOTUNE       0x4u  /* skip the create-time (turns per launch, band) timing
+                                            sweep on large boards (results never depend on it) */
 
 typedef struct gol_config {
     int32_t  width;       /* Params.ImageWidth  (>= 2)                                   */

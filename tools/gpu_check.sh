@@ -26,6 +26,8 @@ for step in "$@"; do
     pmcsq1) run pmcsq1 300 env TAG=_k1 BENCH_ARGS="--tpl 1" bash tools/pmc_sq.sh ;;
     strips) run strips 300 python -u tools/strip_emulate.py ;;
     stripsk) run stripsk 400 python -u tools/strip_emulate.py --halo 120 --tpl 4,6,8 ;;
+    auto)   run auto 400 python -u tools/strip_emulate.py --halo 120 --full ;;
+    auto16k) run auto16k 300 python -u tools/strip_emulate.py --size 16384 --n 2 --halo 120 --full --turns 4800 ;;
     strips8) run strips8 500 python -u tools/strip_emulate.py --n 8 --halo 120 --tpl 1,4,6,8 --band 16,24,32,48,64,96 ;;
     dist)   run t_dist 400 python -u -m pytest tests/test_gpu_distributed.py -v --timeout 300 --timeout-method thread ;;
     tbq)    run tbq 500 python -u tools/sweep.py --variants 2 --bands 0,64,128,137,200,240,274,300,400 --tpl 6,8 --mw 1 --turns 120 ;;

@@ -23,11 +23,29 @@ def main():
     ap.add_argument("--size", type=int, default=65536)
     ap.add_argument("--n", default="2,4,8")
     ap.add_argument("--halo", default="64,128,256")
+    ap.add_argument("--full", action="store_true", help="also time the N=1 torus engine")
     ap.add_argument("--turns", type=int, default=768)
     ap.add_argument("--tpl", default="0")
     ap.add_argument("--band", default="0")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if a.full:
+        e = gol.Engine(a.size, a.size, device=0)
+        e.fill_random(3)
+        s = torch.cuda.Stream()
+        e.set_stream(s.cuda_stream)
+        e.step(16)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        e.step(a.turns)
+        e1.record(s)
+        e1.synchronize()
+        info = e.info()
+        us = e0.elapsed_time(e1) * 1e3 / a.turns
+        print(json.dumps({"n": 1, "rows": a.size, "band": info.band_rows,
+                          "tpl": info.turns_per_launch, "us_per_turn": round(us, 2),
+                          "GCUPS": round(a.size * a.size / us / 1e3, 1)}), flush=True)
+        e.close()
     for n in [int(x) for x in a.n.split(",")]:
         for halo, tpl, band in [(int(h), int(t), int(b)) for h in a.halo.split(",")
                                 for t in a.tpl.split(",") for b in a.band.split(",")]:
