@@ -286,7 +286,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 8 : 6);
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
-    if (!c->fast) c->tpl = 1;
+    if (!c->fast || !golk::multi_fits(c->nw, c->pitch, c->buf_rows)) c->tpl = 1;
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);

@@ -47,6 +47,7 @@ bool fast_path_ok(int width);
 // no counts.  turns in {2, 3, 4, 5, 6, 8}.
 constexpr int kMaxTurnsPerLaunch = 8;
 bool multi_ok(int width, int turns);
+bool multi_fits(int nw, int pitch, int rows);   // buffer addressable with 32-bit dword offsets
 int auto_band_multi(int width, int rows, int words_per_lane);
 // resident 256-thread blocks per CU of k_step_multi<turns, words_per_lane> (0 on error)
 int multi_blocks_per_cu(int turns, int words_per_lane);

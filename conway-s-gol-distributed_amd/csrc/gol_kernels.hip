@@ -423,28 +423,34 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
     const int t0 = tx * STRIDE;                        // first stored word
     const int t1 = min(t0 + STRIDE, nw);               // end of stored words
     const int last = (t1 - t0 + V - 1) / V + 1;        // right halo lane
-    const bool act = lane <= last;
     const bool st = lane >= 1 && lane < last;
+    // every lane loads (its word index wraps mod nw, so lanes past the right halo lane hold
+    // the true torus neighbours): no exec-masked loads; only stores are masked
     int w = t0 - V + V * lane;                         // lane's first word (torus wrap)
     while (w < 0) w += nw;
     while (w >= nw) w -= nw;
-    const size_t pitch32 = (size_t)a.pitch * 2;
+    // dword offsets fit 32 bits: the host only launches this kernel on buffers of
+    // < 2^31 dwords (multi_ok)
+    const uint32_t pitch32 = (uint32_t)a.pitch * 2u;
     const uint32_t *in32 = reinterpret_cast<const uint32_t *>(in) + 2 * (size_t)w;
     uint32_t *out32 = reinterpret_cast<uint32_t *>(out) + 2 * (size_t)w;
     const int M = a.modrows;
-    auto rowoff = [&](int r) -> size_t {     // r in [-K, M + K): may wrap more than once
+    auto rowoff = [&](int r) -> uint32_t {   // r in [-K, M + K): may wrap more than once
         while (r < 0) r += M;
         while (r >= M) r -= M;
-        return (size_t)r * pitch32;
+        return (uint32_t)r * pitch32;
     };
-    auto load = [&](int r, uint32_t (&c)[ND]) {
-        if (act) {
-            vec_get<V>(*reinterpret_cast<const Vec *>(in32 + rowoff(r)), c);
-        } else {
-#pragma unroll
-            for (int k = 0; k < ND; ++k) c[k] = 0;
-        }
+    // Row offsets advance by one row per step: keep them as wave-uniform running values
+    // (a per-step rowoff() of a computed row turned into a VALU urem sequence).
+    const uint32_t span = (uint32_t)M * pitch32;
+    auto adv = [&](uint32_t &o) {
+        o += pitch32;
+        o = o >= span ? o - span : o;
     };
+    auto load_at = [&](uint32_t off, uint32_t (&c)[ND]) {
+        vec_get<V>(*reinterpret_cast<const Vec *>(in32 + off), c);
+    };
+    auto load = [&](int r, uint32_t (&c)[ND]) { load_at(rowoff(r), c); };
     // per stage: ring of 3 row sums and 3 raw input rows (phase = step % 3)
     uint32_t S0[K][3][ND], S1[K][3][ND], X[K][3][ND];
 #pragma unroll
@@ -455,6 +461,8 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
             for (int k = 0; k < ND; ++k) S0[j][p][k] = S1[j][p][k] = X[j][p][k] = 0;
     uint32_t raw[3][ND];
     const int r_first = y0 - K, r_end = y1 + K;         // input rows [r_first, r_end)
+    uint32_t ld_off = rowoff(r_first + 3);              // row prefetched by the next step
+    uint32_t st_off = rowoff(r_first - K);              // row r - K stored by the next step
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
         if (r_first + p < r_end) {
@@ -474,7 +482,8 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
         uint32_t x[ND];
 #pragma unroll
         for (int k = 0; k < ND; ++k) x[k] = raw[pn][k];
-        if (r + 3 < r_end) load(r + 3, raw[pn]);
+        if (r + 3 < r_end) load_at(ld_off, raw[pn]);
+        adv(ld_off);
 #pragma unroll
         for (int j = 0; j < NS; ++j) {
             // row sums of the new input row, dword by dword, each consumed right away by
@@ -503,8 +512,9 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
         }
         if constexpr (NS == K) {
             const int ry = r - K;                        // final output row
-            if (st && ry >= y0) *reinterpret_cast<Vec *>(out32 + rowoff(ry)) = vec_make(x);
+            if (st && ry >= y0) *reinterpret_cast<Vec *>(out32 + st_off) = vec_make(x);
         }
+        adv(st_off);
     };
 
     // Prologue: stage j's first needed output (row y0-K+1+j) comes at step 2j+2 and its
@@ -839,6 +849,12 @@ int auto_band_multi(int width, int rows, int words_per_lane)
 bool multi_ok(int width, int turns)
 {
     return fast_path_ok(width) && turns >= 2 && turns <= kMaxTurnsPerLaunch;
+}
+
+bool multi_fits(int nw, int pitch, int rows)
+{
+    (void)nw;
+    return (long long)rows * pitch * 2 < (1ll << 31);   // 32-bit dword offsets in k_step_multi
 }
 
 template <int V>

@@ -30,8 +30,10 @@ for step in "$@"; do
     auto16k) run auto16k 300 python -u tools/strip_emulate.py --size 16384 --n 2 --halo 120 --full --turns 4800 ;;
     strips8) run strips8 500 python -u tools/strip_emulate.py --n 8 --halo 120 --tpl 1,4,6,8 --band 16,24,32,48,64,96 ;;
     dist)   run t_dist 400 python -u -m pytest tests/test_gpu_distributed.py -v --timeout 300 --timeout-method thread ;;
+    tbk)    run tbk 400 python -u tools/sweep.py --variants 2 --bands 96,137,192 --tpl 6,8 --mw 1 --turns 240 ;;
     tbq)    run tbq 500 python -u tools/sweep.py --variants 2 --bands 0,64,128,137,200,240,274,300,400 --tpl 6,8 --mw 1 --turns 120 ;;
     tbq16k) run tbq16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 0,16,20,24,32,48 --tpl 4,6,8 --mw 1 --turns 960 ;;
+    calib)  run calib 300 bash tools/calib/run.sh ;;
     sweep)  run sweep 400 python -u tools/sweep.py --variants 2,4,5,6 --bands 16,32,64,128,256 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
