@@ -46,6 +46,17 @@ __device__ __forceinline__ uint32_t dpp_from_upper(uint32_t old_v, uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old_v, (int)v, 0x130, 0xf, 0xf, false);
 }
 
+// bound_ctrl forms: the lane without a source (0 / 63) reads 0 -- no `old` operand to
+// materialise (the update_dpp(0, ...) form costs a v_mov per use)
+__device__ __forceinline__ uint32_t dpp_from_lower_z(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t dpp_from_upper_z(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
+}
+
 template <typename T>
 __device__ __forceinline__ T maj3(T a, T b, T c) { return (a & b) | (c & (a | b)); }
 
@@ -488,8 +499,8 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
         for (int j = 0; j < NS; ++j) {
             // row sums of the new input row, dword by dword, each consumed right away by
             // the rule so the oldest row's sums die early (register pressure)
-            const uint32_t L = dpp_from_lower(0u, x[ND - 1]);
-            const uint32_t R = dpp_from_upper(0u, x[0]);
+            const uint32_t L = dpp_from_lower_z(x[ND - 1]);
+            const uint32_t R = dpp_from_upper_z(x[0]);
 #pragma unroll
             for (int k = 0; k < ND; ++k) {
                 const uint32_t wl = __builtin_amdgcn_alignbit(x[k], k == 0 ? L : x[k - 1], 31);
