@@ -47,6 +47,7 @@ struct gol_ctx {
     int variant = golk::kVariantDefault;
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
     int multi_words = 2;                     // k_step_multi words per lane
+    int multi_variant = golk::kMultiSkew;    // temporal-blocking kernel (kMulti*)
     int band_multi = 64;                     // band height of the multi-turn kernel
     float tuned_us_per_turn = 0.f;           // autotune's best measurement (0 = not tuned)
     uint64_t *board[2] = {nullptr, nullptr};
@@ -167,6 +168,7 @@ void autotune_multi(gol_ctx *c, bool tune_k)
     a.cnt_hi = 0;
     a.variant = c->variant;
     a.multi_words = c->multi_words;
+    a.multi_variant = c->multi_variant;
     if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
                                  c->buf_rows, 12345, c->stream) != hipSuccess)
         return;
@@ -282,6 +284,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     // 87 VGPRs at K=4), K = 6 on large boards (64-row bands), K = 4 on smaller ones
     c->multi_words = 1;
     if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
+    if (const char *v = getenv("GOL_MULTI_VARIANT")) {    // A/B experiments only
+        const int k = atoi(v);
+        c->multi_variant = k >= 0 && k < golk::kMultiCount ? k : golk::kMultiSkew;
+    }
     const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
     c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 8 : 6);
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
@@ -294,7 +300,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     if (c->band_multi <= 0 && c->tpl > 1) {
         int ncu = 0;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        const int bpc = golk::multi_blocks_per_cu(c->tpl, c->multi_words);
+        const int bpc = golk::multi_blocks_per_cu(c->tpl, c->multi_words, c->multi_variant);
         c->band_multi = golk::pick_band_multi(cfg->width, cfg->rows, c->multi_words, c->tpl,
                                               ncu * bpc * 4);
     }
@@ -495,6 +501,7 @@ int gol_step(gol_ctx *c, int64_t turns)
     a.band = c->band;
     a.variant = c->variant;
     a.multi_words = c->multi_words;
+    a.multi_variant = c->multi_variant;
     for (int64_t t = 0; t < turns;) {
         // temporal blocking: fuse k turns into one pass when nothing needs per-turn output
         int k = 1;

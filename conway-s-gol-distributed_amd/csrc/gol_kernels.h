@@ -25,6 +25,18 @@ struct StepArgs {
     int band;                          // rows per wavefront (fast) / per thread (generic)
     int variant;                       // fast-path kernel variant (kVariant*)
     int multi_words;                   // k_step_multi words per lane (1 or 2)
+    int multi_variant;                 // temporal-blocking kernel (kMulti*)
+};
+
+// temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkew is shipped)
+enum : int {
+    kMultiSerial = 0,       // k_step_multi: stages chained within a step
+    kMultiSkew = 1,         // k_step_skew: stages one step apart, LDS-DMA prefetch of 8 rows,
+                            //   4 waves/SIMD (V = 1), 7-op rule
+    kMultiSkewPD5 = 2,      // k_step_skew, 5 rows in flight, no wave floor (V = 1, K = 6/8 only)
+    kMultiSkewW1 = 3,       // k_step_skew, no wave floor                   (V = 1, K = 6/8 only)
+    kMultiSkewRule8 = 4,    // k_step_skew with the 8-op rule               (V = 1, K = 6/8 only)
+    kMultiCount = 5,
 };
 
 // fast-path stencil variants (A/B-able in one process; kVariantDefault is shipped)
@@ -49,8 +61,8 @@ constexpr int kMaxTurnsPerLaunch = 8;
 bool multi_ok(int width, int turns);
 bool multi_fits(int nw, int pitch, int rows);   // buffer addressable with 32-bit dword offsets
 int auto_band_multi(int width, int rows, int words_per_lane);
-// resident 256-thread blocks per CU of k_step_multi<turns, words_per_lane> (0 on error)
-int multi_blocks_per_cu(int turns, int words_per_lane);
+// resident 256-thread blocks per CU of the temporal-blocking kernel (0 on error)
+int multi_blocks_per_cu(int turns, int words_per_lane, int variant);
 // band height minimising (residency rounds x per-wavefront work) for the multi kernel
 int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capacity_waves);
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);

@@ -240,6 +240,39 @@ __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c)
     return bitop3<0xe8>(a, b, c);
 }
 
+// B3/S23 from the three rows' 3-cell sums (a, b, c: low bits a0 b0 c0, high bits a1 b1
+// c1; the window's middle row b includes the centre) and the centre bit C.
+// T = L + 2H with L = a0 + b0 + c0, H = a1 + b1 + c1; next = (T == 3) | (C & T == 4).
+// life_rule8: L and H in binary (4 ops), then H' = L/2 + H compared with 1 and 2 (4 ops).
+__device__ __forceinline__ uint32_t life_rule8(uint32_t a0, uint32_t b0, uint32_t c0, uint32_t a1,
+                                               uint32_t b1, uint32_t c1, uint32_t C)
+{
+    const uint32_t u0 = xor3(a0, b0, c0);
+    const uint32_t u1 = maj(a0, b0, c0);
+    const uint32_t v0 = xor3(a1, b1, c1);
+    const uint32_t v1 = maj(a1, b1, c1);
+    const uint32_t h1 = bitop3<0x14>(u1, v0, v1);      // (u1 ^ v0) & ~v1   : H' == 1
+    const uint32_t h2 = bitop3<0x42>(u1, v0, v1);      // H' == 2
+    const uint32_t xx = bitop3<0x08>(u0, C, h2);       // ~u0 & C & h2
+    return bitop3<0xea>(u0, h1, xx);                   // (u0 & h1) | xx
+}
+// life_rule7: 7 ops.  L is encoded as (L >= 2, L in {1,2}) -- majority and "not all
+// equal" of the low bits -- and H as (H >= 2, H odd); the three final LUTs were found by
+// an exhaustive search over 3-gate circuits on those 5 signals (no 2-gate circuit
+// exists for any injective encoding) and are checked on all 512 3x3 windows by
+// tests/test_host_cpu.py::test_rule7_truth_tables.
+__device__ __forceinline__ uint32_t life_rule7(uint32_t a0, uint32_t b0, uint32_t c0, uint32_t a1,
+                                               uint32_t b1, uint32_t c1, uint32_t C)
+{
+    const uint32_t lm = maj(a0, b0, c0);               // L >= 2
+    const uint32_t lx = bitop3<0x7e>(a0, b0, c0);      // L in {1, 2}
+    const uint32_t hm = maj(a1, b1, c1);               // H >= 2
+    const uint32_t hx = xor3(a1, b1, c1);              // H odd
+    const uint32_t g1 = bitop3<0x16>(lm, lx, C);
+    const uint32_t g2 = bitop3<0x86>(hm, C, g1);
+    return bitop3<0x82>(lx, hx, g2);
+}
+
 template <typename F, int... Is>
 __device__ __forceinline__ void unroll_seq(std::integer_sequence<int, Is...>, F &&f)
 {
@@ -253,6 +286,7 @@ struct Slot {
 };
 
 typedef const __attribute__((address_space(4))) uint32_t *const_u32p;
+typedef __attribute__((address_space(3))) void lds_void;
 
 template <bool BLK, bool CNT, int D, bool NT>
 __global__ __launch_bounds__(256) void k_step_ring(const uint64_t *__restrict__ in,
@@ -547,6 +581,213 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
     }
     if (r < r_end) step(std::integral_constant<int, P0>{}, Kc{}, r);
     if (r + 1 < r_end) step(std::integral_constant<int, (P0 + 1) % 3>{}, Kc{}, r + 1);
+}
+
+// ------------------------- K1s: K turns per launch, skewed stage pipeline (the default)
+// Same tiles, halo lanes and bit-sliced rule as k_step_multi; three changes:
+//  * Skew.  Stage j consumes the row stage j-1 produced in the PREVIOUS step, so the K
+//    stages of one step are independent dependency chains (K-wide ILP per wavefront)
+//    instead of one serial chain of ~7K levels.  Stage j outputs row r_first + s - 1 - 2j
+//    at step s; it fills its 3-row window at steps 3j, 3j+1 and computes from 3j+2 on.
+//    All stages share ring phase s % 3.
+//  * Wave-uniform bookkeeping.  The wavefront id goes through readfirstlane, so band,
+//    tile, row offsets and loop control live in SGPRs and branches are scalar; loads are
+//    unconditional (rows past the band wrap in-bounds and feed only unstored outputs).
+//  * LDS-DMA prefetch.  Row s + PD is loaded at the end of step s, by global_load_lds,
+//    into the LDS slot of row s - 1 (a per-wavefront ring of RQ = PD + 1 slots) and read
+//    back with a counted vmcnt wait when stage 0 consumes it.  Register-destination
+//    prefetches became loop-carried register copies that the compiler guarded with
+//    vmcnt waits for every row in flight; LDS slots carry no registers across the loop.
+//    The steady loop is unrolled by U = lcm(3, RQ) so slot offsets are immediates.
+// Steps: prologue [0, 3K-3) with compile-time stage ranges, steady [3K-3, nr) unrolled by
+// U, epilogue K-1 steps (stage j active while j > e).  nr = input rows, padded so the
+// steady part is a multiple of U; rows past r_end feed only outputs >= y1 (not stored).
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+
+template <int K, int V, int PD, int MINW, bool R7>
+__global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restrict__ in,
+                                                   uint64_t *__restrict__ out, StepArgs a,
+                                                   int ntx)
+{
+    static_assert(K >= 2, "one turn per launch is k_step_ring");
+    constexpr int ND = 2 * V;
+    constexpr int STRIDE = 62 * V;
+    constexpr int RQ = PD + 1;                          // prefetch ring slots
+    constexpr int U = 3 * RQ / cgcd(3, RQ);             // steady-loop unroll
+    constexpr int S0_ = 3 * K - 3;                      // first steady step
+    using Vec = typename LaneVec<V>::T;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int tx = wv % ntx;
+    const int by = wv / ntx;
+    const int y0 = a.row_lo + by * a.band;
+    if (y0 >= a.row_hi) return;
+    const int y1 = min(y0 + a.band, a.row_hi);          // stored outputs [y0, y1)
+    int nr = max(y1 - y0, K) + 2 * K;                   // >= S0_ + 3
+    nr = S0_ + (nr - S0_ + U - 1) / U * U;
+
+    const int nw = a.nw;
+    const int t0 = tx * STRIDE;
+    const int t1 = min(t0 + STRIDE, nw);
+    const int last = (t1 - t0 + V - 1) / V + 1;         // right halo lane
+    const bool st = lane >= 1 && lane < last;
+    int w = t0 - V + V * lane;                          // lane's first word (torus wrap)
+    while (w < 0) w += nw;
+    while (w >= nw) w -= nw;
+    const uint32_t lane_b = (uint32_t)w * 8u;
+    // byte offsets fit 32 bits: the host launches this kernel only on buffers < 4 GiB
+    const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
+    const int M = a.modrows;
+    const uint32_t span = (uint32_t)M * pitch_b;
+    auto rowoff = [&](int r) -> uint32_t {
+        while (r < 0) r += M;
+        while (r >= M) r -= M;
+        return (uint32_t)r * pitch_b;
+    };
+    auto adv = [&](uint32_t &o) {
+        o += pitch_b;
+        o = o >= span ? o - span : o;
+    };
+    const char *inb = reinterpret_cast<const char *>(in);
+    char *outb = reinterpret_cast<char *>(out);
+    // prefetch ring in LDS: each wavefront owns RQ row slots of 64 lanes x ND dwords,
+    // filled by LDS-DMA (global_load_lds_dword, dword k of every lane into plane k)
+    __shared__ uint32_t lds_rows[4][RQ][ND][64];
+    uint32_t(*slots)[ND][64] = lds_rows[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
+    auto issue = [&](uint32_t off, auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const uint32_t *g = reinterpret_cast<const uint32_t *>((inb + off) + lane_b);
+#pragma unroll
+        for (int k = 0; k < ND; ++k)
+            __builtin_amdgcn_global_load_lds(g + k, (lds_void *)&slots[q][k][0], 4, 0, 0);
+    };
+    // row in slot q: wait until at most ND*(PD-1) vector-memory ops are outstanding -- the
+    // ND*(PD-1) DMA dwords of the PD-1 later rows were issued after it (stores, when
+    // present, only make the wait earlier), then read it back
+    auto fetch = [&](auto Qc, uint32_t (&c)[ND]) {
+        constexpr int q = decltype(Qc)::value;
+        constexpr int n = ND * (PD - 1);
+        __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
+#pragma unroll
+        for (int k = 0; k < ND; ++k) c[k] = slots[q][k][lane];
+    };
+
+    uint32_t S0[K][3][ND], S1[K][3][ND], X[K][3][ND], XS[K][ND];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+            XS[j][k] = 0;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) S0[j][p][k] = S1[j][p][k] = X[j][p][k] = 0;
+        }
+    uint32_t ld_off = rowoff(y0 - K);                   // input row r_first = y0 - K
+    unroll_seq(std::make_integer_sequence<int, PD>{}, [&](auto Qc) {
+        issue(ld_off, Qc);
+        adv(ld_off);
+    });
+    uint32_t st_off = 0;
+    int ry = 0;                                          // row stage K-1 outputs this step
+
+    // one stage: input row x enters stage j's window at phase P; if RULE, the window's
+    // middle row advances one turn into `o`
+    auto stage = [&](auto Jc, auto Pc, auto RULEc, const uint32_t (&x)[ND], uint32_t (&o)[ND]) {
+        constexpr int j = decltype(Jc)::value;
+        constexpr int P = decltype(Pc)::value;
+        constexpr int pm = (P + 2) % 3, po = (P + 1) % 3;   // middle, oldest row
+        const uint32_t L = dpp_from_lower_z(x[ND - 1]);
+        const uint32_t R = dpp_from_upper_z(x[0]);
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+            const uint32_t wl = __builtin_amdgcn_alignbit(x[k], k == 0 ? L : x[k - 1], 31);
+            const uint32_t er = __builtin_amdgcn_alignbit(k == ND - 1 ? R : x[k + 1], x[k], 1);
+            S0[j][P][k] = xor3(wl, x[k], er);
+            S1[j][P][k] = maj(wl, x[k], er);
+            X[j][P][k] = x[k];
+        }
+        if constexpr (decltype(RULEc)::value) {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                if constexpr (R7)
+                    o[k] = life_rule7(S0[j][po][k], S0[j][pm][k], S0[j][P][k], S1[j][po][k],
+                                      S1[j][pm][k], S1[j][P][k], X[j][pm][k]);
+                else
+                    o[k] = life_rule8(S0[j][po][k], S0[j][pm][k], S0[j][P][k], S1[j][po][k],
+                                      S1[j][pm][k], S1[j][P][k], X[j][pm][k]);
+            }
+        }
+    };
+
+    // step s (compile-time s mod U as SM): stages [JA, JB) active, stages < JR compute the
+    // rule (JR <= JB); LD = stage 0 consumes slot s % RQ and row s + PD is loaded after it.
+    // Stages run in descending order so stage j+1 reads XS[j+1] before stage j rewrites it.
+    auto step = [&](auto SMc, auto JAc, auto JBc, auto JRc, auto LDc) {
+        constexpr int SM = decltype(SMc)::value;
+        constexpr int P = SM % 3;
+        constexpr int JA = decltype(JAc)::value, JB = decltype(JBc)::value;
+        constexpr int JR = decltype(JRc)::value;
+        constexpr bool LD = decltype(LDc)::value;
+        using Pc = std::integral_constant<int, P>;
+        unroll_seq(std::make_integer_sequence<int, JB - JA>{}, [&](auto I) {
+            constexpr int j = JB - 1 - decltype(I)::value;
+            using RULE = std::integral_constant<bool, (j < JR)>;
+            uint32_t x[ND];
+            if constexpr (j == 0) {
+                fetch(std::integral_constant<int, SM % RQ>{}, x);
+            } else {
+#pragma unroll
+                for (int k = 0; k < ND; ++k) x[k] = XS[j][k];
+            }
+            if constexpr (j == K - 1) {
+                uint32_t o[ND];
+                stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, o);
+                if constexpr (RULE::value) {
+                    if (st && ry >= y0 && ry < y1)
+                        *reinterpret_cast<Vec *>((outb + st_off) + lane_b) = vec_make(o);
+                }
+            } else {
+                stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, XS[j + 1]);
+            }
+        });
+        if constexpr (LD) {                             // row s + PD into row s-1's slot
+            issue(ld_off, std::integral_constant<int, (SM + PD) % RQ>{});
+            adv(ld_off);
+        }
+        if constexpr (JR == K) {                         // stage K-1 produced row ry
+            adv(st_off);
+            ++ry;
+        }
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    using Z = std::integral_constant<int, 0>;
+    using Kc = std::integral_constant<int, K>;
+
+    // prologue: steps 0 .. 3K-4
+    unroll_seq(std::make_integer_sequence<int, S0_>{}, [&](auto Sc) {
+        constexpr int s = decltype(Sc)::value;
+        constexpr int JB = s / 3 + 1;
+        constexpr int JR = s >= 2 ? (s - 2) / 3 + 1 : 0;
+        step(std::integral_constant<int, s % U>{}, Z{}, std::integral_constant<int, JB>{},
+             std::integral_constant<int, JR>{}, T{});
+    });
+    // steady state: every stage active; step s outputs row y0 + s - 3K + 1
+    ry = y0 - 2;
+    st_off = rowoff(ry);
+    for (int s = S0_; s < nr; s += U) {
+        unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto Ic) {
+            constexpr int i = decltype(Ic)::value;
+            step(std::integral_constant<int, (S0_ + i) % U>{}, Z{}, Kc{}, Kc{}, T{});
+        });
+    }
+    // epilogue: step nr + e runs stages e+1 .. K-1 (nr == S0_ mod U)
+    unroll_seq(std::make_integer_sequence<int, K - 1>{}, [&](auto Ec) {
+        constexpr int e = decltype(Ec)::value;
+        step(std::integral_constant<int, (S0_ + e) % U>{}, std::integral_constant<int, e + 1>{},
+             Kc{}, Kc{}, F{});
+    });
+    // the last PD prefetches (rows past the band) must land before the LDS is released
+    __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
 }
 
 // ---------------------------------------------------- K1g: generic stencil
@@ -865,7 +1106,72 @@ bool multi_ok(int width, int turns)
 bool multi_fits(int nw, int pitch, int rows)
 {
     (void)nw;
-    return (long long)rows * pitch * 2 < (1ll << 31);   // 32-bit dword offsets in k_step_multi
+    return (long long)rows * pitch * 8 < (1ll << 32);   // 32-bit byte offsets in k_step_skew
+}
+
+// skew-kernel configurations (kMulti* variants): rows in flight, min waves per SIMD
+// (MINW 4 = at most 128 VGPRs: 4 waves per SIMD; only V = 1 fits), rule
+template <int Var, int V> struct SkewCfg;
+template <int V> struct SkewCfg<kMultiSkew, V> {
+    static constexpr int PD = 8, MINW = V == 1 ? 4 : 1;
+    static constexpr bool R7 = true;
+};
+template <int V> struct SkewCfg<kMultiSkewPD5, V> {
+    static constexpr int PD = 5, MINW = 1;
+    static constexpr bool R7 = true;
+};
+template <int V> struct SkewCfg<kMultiSkewW1, V> {
+    static constexpr int PD = 8, MINW = 1;
+    static constexpr bool R7 = true;
+};
+template <int V> struct SkewCfg<kMultiSkewRule8, V> {
+    static constexpr int PD = 8, MINW = V == 1 ? 4 : 1;
+    static constexpr bool R7 = false;
+};
+
+template <int K, int V, int Var>
+static void *skew_fn()
+{
+    using C = SkewCfg<Var, V>;
+    return reinterpret_cast<void *>(&k_step_skew<K, V, C::PD, C::MINW, C::R7>);
+}
+
+// kernel for (turns, words per lane, variant); experimental variants exist for V = 1 and
+// K in {6, 8} only and fall back to kMultiSkew elsewhere
+template <int V>
+static void *multi_fn(int turns, int variant)
+{
+    if (variant == kMultiSerial) {
+        switch (turns) {
+        case 2: return reinterpret_cast<void *>(&k_step_multi<2, V>);
+        case 3: return reinterpret_cast<void *>(&k_step_multi<3, V>);
+        case 4: return reinterpret_cast<void *>(&k_step_multi<4, V>);
+        case 5: return reinterpret_cast<void *>(&k_step_multi<5, V>);
+        case 6: return reinterpret_cast<void *>(&k_step_multi<6, V>);
+        case 8: return reinterpret_cast<void *>(&k_step_multi<8, V>);
+        default: return nullptr;
+        }
+    }
+    if (V == 1 && (turns == 6 || turns == 8)) {
+#define GOL_SKEW_VAR(VAR)                                                                     \
+    case VAR: return turns == 6 ? skew_fn<6, V, VAR>() : skew_fn<8, V, VAR>();
+        switch (variant) {
+            GOL_SKEW_VAR(kMultiSkewPD5)
+            GOL_SKEW_VAR(kMultiSkewW1)
+            GOL_SKEW_VAR(kMultiSkewRule8)
+        default: break;
+        }
+#undef GOL_SKEW_VAR
+    }
+    switch (turns) {
+    case 2: return skew_fn<2, V, kMultiSkew>();
+    case 3: return skew_fn<3, V, kMultiSkew>();
+    case 4: return skew_fn<4, V, kMultiSkew>();
+    case 5: return skew_fn<5, V, kMultiSkew>();
+    case 6: return skew_fn<6, V, kMultiSkew>();
+    case 8: return skew_fn<8, V, kMultiSkew>();
+    default: return nullptr;
+    }
 }
 
 template <int V>
@@ -875,51 +1181,31 @@ static hipError_t launch_multi_v(const StepArgs &a, int turns, hipStream_t s)
     const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
     const long long nwaves = (long long)ntx * nbands;
     const int blocks = (int)((nwaves + 3) / 4);
-#define GOL_MULTI(K)                                                                          \
-    case K:                                                                                   \
-        hipLaunchKernelGGL((k_step_multi<K, V>), dim3(blocks), dim3(256), 0, s, a.in, a.out,  \
-                           a, ntx);                                                           \
-        break;
-    switch (turns) {
-        GOL_MULTI(2)
-        GOL_MULTI(3)
-        GOL_MULTI(4)
-        GOL_MULTI(5)
-        GOL_MULTI(6)
-        GOL_MULTI(8)
-    default:
-        return hipErrorInvalidValue;
-    }
-#undef GOL_MULTI
-    return hipGetLastError();
+    void *fn = multi_fn<V>(turns, a.multi_variant);
+    if (!fn) return hipErrorInvalidValue;
+    StepArgs args = a;
+    const uint64_t *in = a.in;
+    uint64_t *out = a.out;
+    int ntx_arg = ntx;
+    void *params[] = {&in, &out, &args, &ntx_arg};
+    return hipLaunchKernel(fn, dim3(blocks), dim3(256), params, 0, s);
 }
 
 template <int V>
-static int multi_blocks_per_cu_v(int turns)
+static int multi_blocks_per_cu_v(int turns, int variant)
 {
     int blocks = 0;
-    hipError_t e = hipErrorInvalidValue;
-#define GOL_OCC(K)                                                                            \
-    case K:                                                                                   \
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_step_multi<K, V>, 256, 0); \
-        break;
-    switch (turns) {
-        GOL_OCC(2)
-        GOL_OCC(3)
-        GOL_OCC(4)
-        GOL_OCC(5)
-        GOL_OCC(6)
-        GOL_OCC(8)
-    default:
-        break;
-    }
-#undef GOL_OCC
-    return e == hipSuccess ? blocks : 0;
+    void *fn = multi_fn<V>(turns, variant);
+    if (!fn) return 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) == hipSuccess
+               ? blocks
+               : 0;
 }
 
-int multi_blocks_per_cu(int turns, int words_per_lane)
+int multi_blocks_per_cu(int turns, int words_per_lane, int variant)
 {
-    return words_per_lane == 1 ? multi_blocks_per_cu_v<1>(turns) : multi_blocks_per_cu_v<2>(turns);
+    return words_per_lane == 1 ? multi_blocks_per_cu_v<1>(turns, variant)
+                               : multi_blocks_per_cu_v<2>(turns, variant);
 }
 
 int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capacity_waves)

@@ -150,6 +150,25 @@ def test_temporal_blocking(gol, oracle, monkeypatch, mw, tpl, w, h, band, turns)
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("mv", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tpl", [6, 8])
+@pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 17), (384, 3, 8, 11), (8320, 41, 7, 13),
+                                            (16384, 70, 64, 9), (512, 130, 1000, 24),
+                                            (2048, 300, 137, 16)])
+def test_temporal_blocking_variants(gol, oracle, monkeypatch, mv, tpl, w, h, band, turns):
+    """Every temporal-blocking kernel (serial stages; skewed stages with 3, 5 or 8 rows in
+    flight through LDS-DMA; the 4-waves/SIMD build) is bit-exact, incl. bands shorter than
+    K (the skewed pipeline pads them) and tiny tori."""
+    monkeypatch.setenv("GOL_MULTI_WORDS", "1")
+    monkeypatch.setenv("GOL_MULTI_VARIANT", str(mv))
+    with _engine(gol, w, h, band_rows=band, turns_per_launch=tpl) as e:
+        e.fill_random(mv * 1000 + tpl * 31 + w)
+        e.step(turns)
+        got = e.read_packed()
+    want = oracle.bit_run(oracle.gen_random(mv * 1000 + tpl * 31 + w, w, h), w, turns)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("n,K,tpl", [(2, 8, 4), (3, 5, 4), (4, 6, 8), (1, 7, 3)])
 def test_temporal_blocking_strips(gol, oracle, n, K, tpl):
     """Strip engines use the multi-turn pass within each K-turn halo window."""

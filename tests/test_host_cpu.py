@@ -73,3 +73,41 @@ def test_run_requires_native_library(monkeypatch, tmp_path):
     monkeypatch.setattr(N, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(ImportError):
         N.lib()
+
+
+def _kernel_rule(name):
+    """The body of a device rule function in gol_kernels.hip as (dst, op, args) triples."""
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(__file__), "..", "conway-s-gol-distributed_amd",
+                            "csrc", "gol_kernels.hip")).read()
+    body = src[src.index(f"uint32_t {name}("):]
+    body = body[body.index("{") + 1:body.index("\n}")]
+    ops = []
+    for line in body.splitlines():
+        m = re.search(r"(?:const uint32_t (\w+) =|return) (xor3|maj|bitop3<(0x[0-9a-f]+)>)\((\w+), (\w+), (\w+)\)",
+                      line)
+        if m:
+            imm = {"xor3": 0x96, "maj": 0xE8}.get(m.group(2)) or int(m.group(3), 16)
+            ops.append((m.group(1) or "return", imm, m.group(4, 5, 6)))
+    return ops
+
+
+@pytest.mark.parametrize("name", ["life_rule7", "life_rule8"])
+def test_rule_truth_tables(name):
+    """The bit-sliced rules in the HIP source (v_bitop3 immediates, index
+    (src0 << 2) | (src1 << 1) | src2) reproduce calculateNextState
+    (SubServer/distributor.go:178-200) on all 512 3x3 windows."""
+    ops = _kernel_rule(name)
+    assert ops and ops[-1][0] == "return"
+    for m in range(512):
+        cell = [(m >> i) & 1 for i in range(9)]
+        centre = cell[4]
+        n = sum(cell) - centre
+        want = int(n == 3 or (centre == 1 and n == 2))
+        rs = [sum(cell[3 * r:3 * r + 3]) for r in range(3)]
+        env = {"a0": rs[0] & 1, "b0": rs[1] & 1, "c0": rs[2] & 1,
+               "a1": rs[0] >> 1, "b1": rs[1] >> 1, "c1": rs[2] >> 1, "C": centre}
+        for dst, imm, (x, y, z) in ops:
+            env[dst] = (imm >> ((env[x] << 2) | (env[y] << 1) | env[z])) & 1
+        assert env["return"] == want, (name, m)

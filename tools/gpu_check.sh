@@ -33,6 +33,8 @@ for step in "$@"; do
     tbk)    run tbk 400 python -u tools/sweep.py --variants 2 --bands 96,137,192 --tpl 6,8 --mw 1 --turns 240 ;;
     tbq)    run tbq 500 python -u tools/sweep.py --variants 2 --bands 0,64,128,137,200,240,274,300,400 --tpl 6,8 --mw 1 --turns 120 ;;
     tbq16k) run tbq16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 0,16,20,24,32,48 --tpl 4,6,8 --mw 1 --turns 960 ;;
+    skew)   run skew 500 python -u tools/sweep.py --variants 2 --bands 96,137,192 --tpl 6,8 --mw 1 --mv 0,1,2,3,4 --turns 240 ;;
+    skew16k) run skew16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 16,20,24,32 --tpl 6,8 --mw 1 --mv 0,1,2,3,4 --turns 960 ;;
     calib)  run calib 300 bash tools/calib/run.sh ;;
     sweep)  run sweep 400 python -u tools/sweep.py --variants 2,4,5,6 --bands 16,32,64,128,256 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;

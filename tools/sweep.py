@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--bands", default="0,32,64,128")
     ap.add_argument("--tpl", default="1", help="turns per launch values")
     ap.add_argument("--mw", default="2", help="k_step_multi words per lane values")
+    ap.add_argument("--mv", default="1", help="temporal-blocking kernel variants (kMulti*)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     W, H = a.size, a.height or a.size
@@ -35,13 +36,15 @@ def main():
         for b in [int(x) for x in a.bands.split(",")]:
             for k in [int(x) for x in a.tpl.split(",")]:
                 for mw in ([int(x) for x in a.mw.split(",")] if k > 1 else [2]):
-                    os.environ["GOL_STENCIL_VARIANT"] = str(v)
-                    os.environ["GOL_MULTI_WORDS"] = str(mw)
-                    e = gol.Engine(W, H, device=0, band_rows=b, turns_per_launch=k)
-                    e.set_stream(stream.cuda_stream)
-                    e.fill_random(3)
-                    e.step(5)
-                    engines[(v, e.info().band_rows, k, mw)] = e
+                    for mv in ([int(x) for x in a.mv.split(",")] if k > 1 else [1]):
+                        os.environ["GOL_STENCIL_VARIANT"] = str(v)
+                        os.environ["GOL_MULTI_WORDS"] = str(mw)
+                        os.environ["GOL_MULTI_VARIANT"] = str(mv)
+                        e = gol.Engine(W, H, device=0, band_rows=b, turns_per_launch=k)
+                        e.set_stream(stream.cuda_stream)
+                        e.fill_random(3)
+                        e.step(5)
+                        engines[(v, e.info().band_rows, k, mw, mv)] = e
     torch.cuda.synchronize()
     res = {k: [] for k in engines}
     for _ in range(a.rounds):
@@ -58,7 +61,7 @@ def main():
     for k, ts in res.items():
         us = statistics.median(ts)
         gbs = 0.25 * W * H / (us * 1e-6) / 1e9
-        out.append({"variant": k[0], "band": k[1], "tpl": k[2], "mw": k[3],
+        out.append({"variant": k[0], "band": k[1], "tpl": k[2], "mw": k[3], "mv": k[4],
                     "us_per_turn": round(us, 2),
                     "min_us": round(min(ts), 2), "GBs": round(gbs, 1),
                     "GCUPS": round(W * H / us / 1e3, 1)})
