@@ -47,11 +47,12 @@ struct gol_ctx {
     int variant = golk::kVariantDefault;
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
     int multi_words = 2;                     // k_step_multi words per lane
-    int multi_variant = golk::kMultiSkew;    // temporal-blocking kernel (kMulti*)
+    int multi_variant = golk::kMultiSkewIL;  // temporal-blocking kernel (kMulti*)
     int band_multi = 64;                     // band height of the multi-turn kernel
     float tuned_us_per_turn = 0.f;           // autotune's best measurement (0 = not tuned)
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
+    bool il = false;                         // board[cur] is in the interleaved layout
     uint64_t *blocked = nullptr;
     bool blocked_pending = false;
     long long nonbinary = 0;
@@ -128,6 +129,22 @@ void release_blocked(gol_ctx *c)
     if (c->blocked) (void)hipFree(c->blocked);
     c->blocked = nullptr;
     c->blocked_pending = false;
+}
+
+// The temporal-blocking kernel runs on the interleaved word layout (gol_kernels.h,
+// multi_is_il); everything else -- the k = 1 stencils, PGM pack/unpack, the alive list,
+// reads, loads, halo rows crossing the API -- sees the standard layout.  The engine
+// converts lazily, whole buffer, when the next consumer needs the other layout (one read
+// and one write of the board: at most twice per gol_step, never inside a run of
+// multi-turn launches).  Popcounts do not depend on the layout.
+int ensure_layout(gol_ctx *c, bool il)
+{
+    if (c->il == il) return GOL_OK;
+    HIP_OR_FAIL(c, golk::launch_il_convert(c->board[c->cur], c->pitch, c->board[c->cur ^ 1],
+                                           c->pitch, c->buf_rows, c->nw, il, c->stream));
+    c->cur ^= 1;
+    c->il = il;
+    return GOL_OK;
 }
 
 // popcount of owned rows of the current board -> *alive (synchronous)
@@ -288,7 +305,8 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         const int k = atoi(v);
         c->multi_variant = k >= 0 && k < golk::kMultiCount ? k : golk::kMultiSkew;
     }
-    const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
+    const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
+    const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
     c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 8 : 6);
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
@@ -301,10 +319,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         int ncu = 0;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         const int bpc = golk::multi_blocks_per_cu(c->tpl, c->multi_words, c->multi_variant);
-        c->band_multi = golk::pick_band_multi(cfg->width, cfg->rows, c->multi_words, c->tpl,
+        c->band_multi = golk::pick_band_multi(cfg->width, cfg->rows, lane_dw, c->tpl,
                                               ncu * bpc * 4);
     }
-    if (c->band_multi <= 0) c->band_multi = golk::auto_band_multi(cfg->width, cfg->rows, c->multi_words);
+    if (c->band_multi <= 0) c->band_multi = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
     const size_t words = (size_t)c->buf_rows * c->pitch;
     int rc = GOL_OK;
     auto bail = [&](int code) {
@@ -428,6 +446,7 @@ int gol_load(gol_ctx *c, const uint8_t *bytes)
     for (int i = 0; i < kShards; i++) s += c->h_counts[i];
     c->nonbinary = (long long)s;
     c->cur = 0;
+    c->il = false;
     c->turn = 0;
     c->launches = 0;
     c->halo_valid = c->cfg.halo;
@@ -455,6 +474,7 @@ int gol_load_packed(gol_ctx *c, const uint64_t *words)
                                     c->stream));
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
+    c->il = false;
     c->turn = 0;
     c->launches = 0;
     c->nonbinary = 0;
@@ -474,6 +494,7 @@ int gol_fill_random(gol_ctx *c, uint64_t seed)
                                             c->buf_rows, grow0, c->cfg.height, seed, c->stream));
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
+    c->il = false;
     c->turn = 0;
     c->launches = 0;
     c->nonbinary = 0;
@@ -520,6 +541,11 @@ int gol_step(gol_ctx *c, int64_t turns)
         } else {
             a.row_lo = 0;
             a.row_hi = c->buf_rows;
+        }
+        {
+            const int rc = ensure_layout(c, k > 1 && golk::multi_is_il(c->multi_words,
+                                                                        c->multi_variant));
+            if (rc) return rc;
         }
         a.in = c->board[c->cur];
         a.out = c->board[c->cur ^ 1];
@@ -611,6 +637,7 @@ int gol_read_board(gol_ctx *c, uint8_t *out)
         return GOL_OK;
     }
     DeviceGuard g(c->device);
+    if (int rc_ = ensure_layout(c, false)) return rc_;
     const int chunk_rows = (int)std::max<size_t>(
         1, std::min<size_t>(kStagingBytes / row_bytes, (size_t)c->cfg.rows));
     int rc = ensure_staging(c, (size_t)chunk_rows * row_bytes);
@@ -631,6 +658,7 @@ int gol_read_packed(gol_ctx *c, uint64_t *out)
     if (!c || !out) return GOL_EINVAL;
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
+    if (int rc_ = ensure_layout(c, false)) return rc_;
     HIP_OR_FAIL(c, hipMemcpy2DAsync(out, (size_t)c->nw * 8,
                                     c->board[c->cur] + (size_t)own_lo(c) * c->pitch,
                                     (size_t)c->pitch * 8, (size_t)c->nw * 8, c->cfg.rows,
@@ -644,6 +672,7 @@ int gol_alive_cells(gol_ctx *c, int64_t *xy, int64_t cap, int64_t *n)
     if (!c || !n || cap < 0 || (cap > 0 && !xy)) return GOL_EINVAL;
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
+    if (int rc_ = ensure_layout(c, false)) return rc_;
     const int rows = c->cfg.rows;
     std::vector<long long> rc((size_t)rows), off((size_t)rows);
     long long *d_rc = nullptr;
@@ -722,6 +751,13 @@ int gol_export_halo(gol_ctx *c, void *top, void *bottom, void *s)
     const int K = c->cfg.halo;
     const size_t rowb = (size_t)c->nw * 8;
     const uint64_t *b = c->board[c->cur];
+    if (c->il) {   // halo rows cross the API in the standard layout
+        HIP_OR_FAIL(c, golk::launch_il_convert(b + (size_t)own_lo(c) * c->pitch, c->pitch,
+                                               (uint64_t *)top, c->nw, K, c->nw, false, st));
+        HIP_OR_FAIL(c, golk::launch_il_convert(b + (size_t)(own_hi(c) - K) * c->pitch, c->pitch,
+                                               (uint64_t *)bottom, c->nw, K, c->nw, false, st));
+        return GOL_OK;
+    }
     HIP_OR_FAIL(c, hipMemcpy2DAsync(top, rowb, b + (size_t)own_lo(c) * c->pitch,
                                     (size_t)c->pitch * 8, rowb, K, hipMemcpyDeviceToDevice, st));
     HIP_OR_FAIL(c, hipMemcpy2DAsync(bottom, rowb, b + (size_t)(own_hi(c) - K) * c->pitch,
@@ -739,10 +775,18 @@ int gol_import_halo(gol_ctx *c, const void *top, const void *bottom, void *s)
     const int K = c->cfg.halo;
     const size_t rowb = (size_t)c->nw * 8;
     uint64_t *b = c->board[c->cur];
-    HIP_OR_FAIL(c, hipMemcpy2DAsync(b, (size_t)c->pitch * 8, top, rowb, rowb, K,
-                                    hipMemcpyDeviceToDevice, st));
-    HIP_OR_FAIL(c, hipMemcpy2DAsync(b + (size_t)own_hi(c) * c->pitch, (size_t)c->pitch * 8,
-                                    bottom, rowb, rowb, K, hipMemcpyDeviceToDevice, st));
+    if (c->il) {
+        HIP_OR_FAIL(c, golk::launch_il_convert((const uint64_t *)top, c->nw, b, c->pitch, K, c->nw,
+                                               true, st));
+        HIP_OR_FAIL(c, golk::launch_il_convert((const uint64_t *)bottom, c->nw,
+                                               b + (size_t)own_hi(c) * c->pitch, c->pitch, K,
+                                               c->nw, true, st));
+    } else {
+        HIP_OR_FAIL(c, hipMemcpy2DAsync(b, (size_t)c->pitch * 8, top, rowb, rowb, K,
+                                        hipMemcpyDeviceToDevice, st));
+        HIP_OR_FAIL(c, hipMemcpy2DAsync(b + (size_t)own_hi(c) * c->pitch, (size_t)c->pitch * 8,
+                                        bottom, rowb, rowb, K, hipMemcpyDeviceToDevice, st));
+    }
     if (st != c->stream) {
         hipEvent_t ev;
         HIP_OR_FAIL(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -757,6 +801,10 @@ int gol_import_halo(gol_ctx *c, const void *top, const void *bottom, void *s)
 static int copy_rows_between(gol_ctx *dst, int dst_row, gol_ctx *src, int src_row, int K)
 {
     if (dst->nw != src->nw) return fail(dst, GOL_EINVAL, "width mismatch");
+    if (src->il != dst->il) {   // raw row copies need one layout on both sides
+        DeviceGuard gs(src->device);
+        if (int rc = ensure_layout(src, dst->il)) return rc;
+    }
     // dst stream waits for src's queued work; copy on dst's stream
     hipEvent_t ev;
     {

@@ -28,15 +28,17 @@ struct StepArgs {
     int multi_variant;                 // temporal-blocking kernel (kMulti*)
 };
 
-// temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkew is shipped)
+// temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkewIL is shipped)
 enum : int {
     kMultiSerial = 0,       // k_step_multi: stages chained within a step
     kMultiSkew = 1,         // k_step_skew: stages one step apart, LDS-DMA prefetch of 8 rows,
-                            //   4 waves/SIMD (V = 1), 7-op rule
+                            //   4 waves/SIMD (V = 1, K < 8; 3 at K = 8), 7-op rule
     kMultiSkewPD5 = 2,      // k_step_skew, 5 rows in flight, no wave floor (V = 1, K = 6/8 only)
     kMultiSkewW1 = 3,       // k_step_skew, no wave floor                   (V = 1, K = 6/8 only)
     kMultiSkewRule8 = 4,    // k_step_skew with the 8-op rule               (V = 1, K = 6/8 only)
-    kMultiCount = 5,
+    kMultiSkewD1 = 5,       // k_step_skew, 1 dword (32 cells) per lane     (V = 1, K = 4/6/8 only)
+    kMultiSkewIL = 6,       // k_step_skew on the interleaved board layout (V = 1; the default)
+    kMultiCount = 7,
 };
 
 // fast-path stencil variants (A/B-able in one process; kVariantDefault is shipped)
@@ -60,11 +62,18 @@ bool fast_path_ok(int width);
 constexpr int kMaxTurnsPerLaunch = 8;
 bool multi_ok(int width, int turns);
 bool multi_fits(int nw, int pitch, int rows);   // buffer addressable with 32-bit dword offsets
-int auto_band_multi(int width, int rows, int words_per_lane);
+// the temporal-blocking kernel for (words per lane, variant) runs on the interleaved layout
+bool multi_is_il(int words_per_lane, int variant);
+// standard <-> interleaved rows (row pitches in words; in and out may not alias)
+hipError_t launch_il_convert(const uint64_t *in, int in_pitch, uint64_t *out, int out_pitch,
+                             int nrows, int nw, bool to_il, hipStream_t s);
+// dwords per lane of the temporal-blocking kernel (tiles advance by 62 x that many dwords)
+int multi_lane_dwords(int words_per_lane, int variant);
+int auto_band_multi(int width, int rows, int lane_dwords);
 // resident 256-thread blocks per CU of the temporal-blocking kernel (0 on error)
 int multi_blocks_per_cu(int turns, int words_per_lane, int variant);
 // band height minimising (residency rounds x per-wavefront work) for the multi kernel
-int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capacity_waves);
+int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacity_waves);
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);

@@ -604,18 +604,32 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
 // steady part is a multiple of U; rows past r_end feed only outputs >= y1 (not stored).
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 
-template <int K, int V, int PD, int MINW, bool R7>
+template <int ND> struct LaneDw;
+template <> struct LaneDw<1> { using T = uint32_t; };
+template <> struct LaneDw<2> { using T = uint2; };
+template <> struct LaneDw<4> { using T = uint4; };
+__device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[0]; }
+
+// ND = dwords per lane (1, 2 or 4: 32, 64 or 128 cells); tiles advance by 62 * ND dwords.
+// IL: the lane's 32 * ND cells are stored interleaved -- dword r holds the cells whose
+// offset in the lane's range is = r (mod ND), bit i <-> offset ND * i + r (the engine's
+// interleaved board layout, il_lane_dwords == ND).  Then the west neighbours of dword r
+// are dword r - 1 as is and the east neighbours dword r + 1 as is; only dword 0's west
+// and dword ND-1's east need a 1-bit funnel shift (v_alignbit, half-rate on gfx950 like
+// DPP: tools/calib/valu_issue.hip), i.e. 2 instead of 2 * ND shifts per lane-row.
+// (ND == 1 makes both layouts the same.)
+template <int K, int ND, int PD, int MINW, bool R7, bool IL = false>
 __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, StepArgs a,
                                                    int ntx)
 {
     static_assert(K >= 2, "one turn per launch is k_step_ring");
-    constexpr int ND = 2 * V;
-    constexpr int STRIDE = 62 * V;
+    static_assert(K <= 32 * ND, "the edge error must stay inside the halo lanes");
+    constexpr int STRIDE = 62 * ND;                     // stored dwords per tile
     constexpr int RQ = PD + 1;                          // prefetch ring slots
     constexpr int U = 3 * RQ / cgcd(3, RQ);             // steady-loop unroll
     constexpr int S0_ = 3 * K - 3;                      // first steady step
-    using Vec = typename LaneVec<V>::T;
+    using Vec = typename LaneDw<ND>::T;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     const int tx = wv % ntx;
@@ -626,15 +640,15 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
     int nr = max(y1 - y0, K) + 2 * K;                   // >= S0_ + 3
     nr = S0_ + (nr - S0_ + U - 1) / U * U;
 
-    const int nw = a.nw;
+    const int nd = 2 * a.nw;                            // dwords per row
     const int t0 = tx * STRIDE;
-    const int t1 = min(t0 + STRIDE, nw);
-    const int last = (t1 - t0 + V - 1) / V + 1;         // right halo lane
+    const int t1 = min(t0 + STRIDE, nd);
+    const int last = (t1 - t0 + ND - 1) / ND + 1;       // right halo lane
     const bool st = lane >= 1 && lane < last;
-    int w = t0 - V + V * lane;                          // lane's first word (torus wrap)
-    while (w < 0) w += nw;
-    while (w >= nw) w -= nw;
-    const uint32_t lane_b = (uint32_t)w * 8u;
+    int w = t0 - ND + ND * lane;                        // lane's first dword (torus wrap)
+    while (w < 0) w += nd;
+    while (w >= nd) w -= nd;
+    const uint32_t lane_b = (uint32_t)w * 4u;
     // byte offsets fit 32 bits: the host launches this kernel only on buffers < 4 GiB
     const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
     const int M = a.modrows;
@@ -699,8 +713,14 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
         const uint32_t R = dpp_from_upper_z(x[0]);
 #pragma unroll
         for (int k = 0; k < ND; ++k) {
-            const uint32_t wl = __builtin_amdgcn_alignbit(x[k], k == 0 ? L : x[k - 1], 31);
-            const uint32_t er = __builtin_amdgcn_alignbit(k == ND - 1 ? R : x[k + 1], x[k], 1);
+            uint32_t wl, er;
+            if constexpr (IL) {
+                wl = k == 0 ? __builtin_amdgcn_alignbit(x[ND - 1], L, 31) : x[k - 1];
+                er = k == ND - 1 ? __builtin_amdgcn_alignbit(R, x[0], 1) : x[k + 1];
+            } else {
+                wl = __builtin_amdgcn_alignbit(x[k], k == 0 ? L : x[k - 1], 31);
+                er = __builtin_amdgcn_alignbit(k == ND - 1 ? R : x[k + 1], x[k], 1);
+            }
             S0[j][P][k] = xor3(wl, x[k], er);
             S1[j][P][k] = maj(wl, x[k], er);
             X[j][P][k] = x[k];
@@ -944,6 +964,47 @@ __global__ __launch_bounds__(256) void k_fill_random(uint64_t *__restrict__ word
 }
 
 // ------------------------------------------------------- K3: alive list
+// ------------------------------------------- layout: standard <-> interleaved words
+// The interleaved layout (k_step_skew<IL>, 2 dwords per lane) keeps each 64-cell word's
+// even cells in its low dword (cell 2i -> bit i) and its odd cells in the high dword
+// (cell 2i+1 -> bit 32+i): the inverse perfect shuffle, five delta swaps (Hacker's
+// Delight 7-2).  Row pitches are in words; one thread per word, grid-stride.
+__device__ __forceinline__ uint64_t dswap(uint64_t x, int s, uint64_t m)
+{
+    const uint64_t t = (x ^ (x >> s)) & m;
+    return x ^ t ^ (t << s);
+}
+__device__ __forceinline__ uint64_t il_unshuffle(uint64_t x)
+{
+    x = dswap(x, 1, 0x2222222222222222ull);
+    x = dswap(x, 2, 0x0C0C0C0C0C0C0C0Cull);
+    x = dswap(x, 4, 0x00F000F000F000F0ull);
+    x = dswap(x, 8, 0x0000FF000000FF00ull);
+    return dswap(x, 16, 0x00000000FFFF0000ull);
+}
+__device__ __forceinline__ uint64_t il_shuffle(uint64_t x)
+{
+    x = dswap(x, 16, 0x00000000FFFF0000ull);
+    x = dswap(x, 8, 0x0000FF000000FF00ull);
+    x = dswap(x, 4, 0x00F000F000F000F0ull);
+    x = dswap(x, 2, 0x0C0C0C0C0C0C0C0Cull);
+    return dswap(x, 1, 0x2222222222222222ull);
+}
+
+template <bool TO_IL>
+__global__ __launch_bounds__(256) void k_il_convert(const uint64_t *__restrict__ in, int in_pitch,
+                                                    uint64_t *__restrict__ out, int out_pitch,
+                                                    int nrows, int nw)
+{
+    const long long total = (long long)nrows * nw;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int r = (int)(i / nw), j = (int)(i % nw);
+        const uint64_t v = in[(size_t)r * in_pitch + j];
+        out[(size_t)r * out_pitch + j] = TO_IL ? il_unshuffle(v) : il_shuffle(v);
+    }
+}
+
 // One wavefront per row.
 __global__ __launch_bounds__(256) void k_row_popcount(const uint64_t *__restrict__ w, int nw,
                                                       int pitch, int row0, int nrows,
@@ -1086,13 +1147,27 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
     return hipGetLastError();
 }
 
-int auto_band_multi(int width, int rows, int words_per_lane)
+bool multi_is_il(int words_per_lane, int variant)
 {
-    const int nw = (width + 63) / 64;
-    const long long ntx = (nw + 62 * words_per_lane - 1) / (62 * words_per_lane);
+    return variant == kMultiSkewIL && words_per_lane == 1;
+}
+
+int multi_lane_dwords(int words_per_lane, int variant)
+{
+    return variant == kMultiSkewD1 ? 1 : 2 * words_per_lane;
+}
+
+static inline long long multi_tiles(int width, int lane_dwords)
+{
+    const long long nd = 2ll * ((width + 63) / 64);
+    return (nd + 62 * lane_dwords - 1) / (62 * lane_dwords);
+}
+
+int auto_band_multi(int width, int rows, int lane_dwords)
+{
     // a band re-reads 2K halo rows and runs 2K pipeline fill steps, so bands are taller
     // than for k=1: 64 rows at 65536^2 (9216 wavefronts), 16 at 16384^2 (measured).
-    long long b = (long long)rows * ntx / 9216;
+    long long b = (long long)rows * multi_tiles(width, lane_dwords) / 9216;
     if (b < 16) b = 16;
     if (b > 64) b = 64;
     return (int)b;
@@ -1110,34 +1185,46 @@ bool multi_fits(int nw, int pitch, int rows)
 }
 
 // skew-kernel configurations (kMulti* variants): rows in flight, min waves per SIMD
-// (MINW 4 = at most 128 VGPRs: 4 waves per SIMD; only V = 1 fits), rule
-template <int Var, int V> struct SkewCfg;
-template <int V> struct SkewCfg<kMultiSkew, V> {
-    static constexpr int PD = 8, MINW = V == 1 ? 4 : 1;
+// (MINW 4 = at most 128 VGPRs: 4 waves per SIMD; only 2 dwords per lane at K < 8 fits
+// without spills -- K = 8 needs 132 VGPRs, and forcing 128 spilled and ran 17 % slower)
+template <int Var, int K, int ND> struct SkewCfg;
+template <int K, int ND> struct SkewCfg<kMultiSkew, K, ND> {
+    static constexpr int PD = 8, MINW = (ND == 2 && K < 8) ? 4 : 1;
     static constexpr bool R7 = true;
 };
-template <int V> struct SkewCfg<kMultiSkewPD5, V> {
+template <int K, int ND> struct SkewCfg<kMultiSkewPD5, K, ND> {
     static constexpr int PD = 5, MINW = 1;
     static constexpr bool R7 = true;
 };
-template <int V> struct SkewCfg<kMultiSkewW1, V> {
+template <int K, int ND> struct SkewCfg<kMultiSkewW1, K, ND> {
     static constexpr int PD = 8, MINW = 1;
     static constexpr bool R7 = true;
 };
-template <int V> struct SkewCfg<kMultiSkewRule8, V> {
-    static constexpr int PD = 8, MINW = V == 1 ? 4 : 1;
+template <int K, int ND> struct SkewCfg<kMultiSkewRule8, K, ND> {
+    static constexpr int PD = 8, MINW = ND == 2 ? 4 : 1;
     static constexpr bool R7 = false;
 };
+template <int K, int ND> struct SkewCfg<kMultiSkewD1, K, ND> {
+    static constexpr int PD = 8, MINW = 1;
+    static constexpr bool R7 = true;
+};
+// the interleaved build at K = 8 wants 129 VGPRs; capped at 128 (4 waves/SIMD) it spills 2
+// outside the steady loop and ran 37.1 vs 40.2 us/turn at 3 waves/SIMD (65536^2, band 274)
+template <int K, int ND> struct SkewCfg<kMultiSkewIL, K, ND> {
+    static constexpr int PD = 8, MINW = 4;
+    static constexpr bool R7 = true;
+};
 
-template <int K, int V, int Var>
+template <int K, int ND, int Var>
 static void *skew_fn()
 {
-    using C = SkewCfg<Var, V>;
-    return reinterpret_cast<void *>(&k_step_skew<K, V, C::PD, C::MINW, C::R7>);
+    using C = SkewCfg<Var, K, ND>;
+    return reinterpret_cast<void *>(
+        &k_step_skew<K, ND, C::PD, C::MINW, C::R7, Var == kMultiSkewIL>);
 }
 
 // kernel for (turns, words per lane, variant); experimental variants exist for V = 1 and
-// K in {6, 8} only and fall back to kMultiSkew elsewhere
+// K in {6, 8} only (kMultiSkewD1: K in {4, 6, 8}) and fall back to kMultiSkew elsewhere
 template <int V>
 static void *multi_fn(int turns, int variant)
 {
@@ -1152,9 +1239,28 @@ static void *multi_fn(int turns, int variant)
         default: return nullptr;
         }
     }
+    if (V == 1 && variant == kMultiSkewIL) {
+        switch (turns) {
+        case 2: return skew_fn<2, 2, kMultiSkewIL>();
+        case 3: return skew_fn<3, 2, kMultiSkewIL>();
+        case 4: return skew_fn<4, 2, kMultiSkewIL>();
+        case 5: return skew_fn<5, 2, kMultiSkewIL>();
+        case 6: return skew_fn<6, 2, kMultiSkewIL>();
+        case 8: return skew_fn<8, 2, kMultiSkewIL>();
+        default: return nullptr;
+        }
+    }
+    if (V == 1 && variant == kMultiSkewD1) {
+        switch (turns) {
+        case 4: return skew_fn<4, 1, kMultiSkewD1>();
+        case 6: return skew_fn<6, 1, kMultiSkewD1>();
+        case 8: return skew_fn<8, 1, kMultiSkewD1>();
+        default: return nullptr;
+        }
+    }
     if (V == 1 && (turns == 6 || turns == 8)) {
 #define GOL_SKEW_VAR(VAR)                                                                     \
-    case VAR: return turns == 6 ? skew_fn<6, V, VAR>() : skew_fn<8, V, VAR>();
+    case VAR: return turns == 6 ? skew_fn<6, 2, VAR>() : skew_fn<8, 2, VAR>();
         switch (variant) {
             GOL_SKEW_VAR(kMultiSkewPD5)
             GOL_SKEW_VAR(kMultiSkewW1)
@@ -1164,12 +1270,12 @@ static void *multi_fn(int turns, int variant)
 #undef GOL_SKEW_VAR
     }
     switch (turns) {
-    case 2: return skew_fn<2, V, kMultiSkew>();
-    case 3: return skew_fn<3, V, kMultiSkew>();
-    case 4: return skew_fn<4, V, kMultiSkew>();
-    case 5: return skew_fn<5, V, kMultiSkew>();
-    case 6: return skew_fn<6, V, kMultiSkew>();
-    case 8: return skew_fn<8, V, kMultiSkew>();
+    case 2: return skew_fn<2, 2 * V, kMultiSkew>();
+    case 3: return skew_fn<3, 2 * V, kMultiSkew>();
+    case 4: return skew_fn<4, 2 * V, kMultiSkew>();
+    case 5: return skew_fn<5, 2 * V, kMultiSkew>();
+    case 6: return skew_fn<6, 2 * V, kMultiSkew>();
+    case 8: return skew_fn<8, 2 * V, kMultiSkew>();
     default: return nullptr;
     }
 }
@@ -1177,11 +1283,15 @@ static void *multi_fn(int turns, int variant)
 template <int V>
 static hipError_t launch_multi_v(const StepArgs &a, int turns, hipStream_t s)
 {
-    const int ntx = (a.nw + 62 * V - 1) / (62 * V);
+    int var = a.multi_variant;                          // depths D1 lacks: 2 dwords per lane
+    if (var == kMultiSkewD1 && !(V == 1 && (turns == 4 || turns == 6 || turns == 8)))
+        var = kMultiSkew;
+    if (var == kMultiSkewIL && V != 1) var = kMultiSkew; // multi_is_il() is false for V = 2
+    const int ntx = (int)multi_tiles(a.width, multi_lane_dwords(V, var));
     const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
     const long long nwaves = (long long)ntx * nbands;
     const int blocks = (int)((nwaves + 3) / 4);
-    void *fn = multi_fn<V>(turns, a.multi_variant);
+    void *fn = multi_fn<V>(turns, var);
     if (!fn) return hipErrorInvalidValue;
     StepArgs args = a;
     const uint64_t *in = a.in;
@@ -1208,7 +1318,7 @@ int multi_blocks_per_cu(int turns, int words_per_lane, int variant)
                                : multi_blocks_per_cu_v<2>(turns, variant);
 }
 
-int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capacity_waves)
+int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacity_waves)
 {
     // Every wavefront of a launch does the same work, so a launch takes ~ rounds x
     // (per-wavefront time), rounds = ceil(waves / resident capacity): a grid that spills
@@ -1218,9 +1328,8 @@ int pick_band_multi(int width, int rows, int words_per_lane, int turns, int capa
     // minimises rounds x per-wave time, charging at least 2 rounds (a single round that
     // starts and ends every wavefront together measured slower: 65536^2 K=6 band 274 vs
     // 137, 60.6 vs 58.0 us/turn); ties go to the smaller band.
-    const int nw = (width + 63) / 64;
-    const long long ntx = (nw + 62 * words_per_lane - 1) / (62 * words_per_lane);
-    if (capacity_waves <= 0) return auto_band_multi(width, rows, words_per_lane);
+    const long long ntx = multi_tiles(width, lane_dwords);
+    if (capacity_waves <= 0) return auto_band_multi(width, rows, lane_dwords);
     long long best_cost = -1;
     int best = 16;
     for (int band = 16; band <= 1024; ++band) {
@@ -1269,6 +1378,20 @@ hipError_t launch_unpack(const uint64_t *words, int width, int nw, int pitch, in
     const int g = grid_for((long long)nrows * nw);
     hipLaunchKernelGGL(k_unpack, dim3(g), dim3(256), 0, s, words, width, nw, pitch, row0, nrows,
                        bytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_il_convert(const uint64_t *in, int in_pitch, uint64_t *out, int out_pitch,
+                             int nrows, int nw, bool to_il, hipStream_t s)
+{
+    if (nrows <= 0) return hipSuccess;
+    const int g = grid_for((long long)nrows * nw);
+    if (to_il)
+        hipLaunchKernelGGL(k_il_convert<true>, dim3(g), dim3(256), 0, s, in, in_pitch, out,
+                           out_pitch, nrows, nw);
+    else
+        hipLaunchKernelGGL(k_il_convert<false>, dim3(g), dim3(256), 0, s, in, in_pitch, out,
+                           out_pitch, nrows, nw);
     return hipGetLastError();
 }
 

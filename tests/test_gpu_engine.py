@@ -150,7 +150,7 @@ def test_temporal_blocking(gol, oracle, monkeypatch, mw, tpl, w, h, band, turns)
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("mv", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("mv", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("tpl", [6, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 17), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (512, 130, 1000, 24),
@@ -167,6 +167,70 @@ def test_temporal_blocking_variants(gol, oracle, monkeypatch, mv, tpl, w, h, ban
         got = e.read_packed()
     want = oracle.bit_run(oracle.gen_random(mv * 1000 + tpl * 31 + w, w, h), w, turns)
     assert np.array_equal(got, want)
+
+
+def il_layout(words, nd, inverse=False):
+    """Packed rows <-> the interleaved layout of k_step_skew<IL> (nd dwords per lane: dword r
+    of a 32*nd-cell lane group holds the cells at offsets = r mod nd, bit i <-> nd*i + r)."""
+    w = np.ascontiguousarray(words, dtype=np.uint64)
+    H, nw = w.shape
+    bits = np.unpackbits(w.view(np.uint8), axis=1, bitorder="little")
+    g = bits.reshape(H, nw * 64 // (32 * nd), 32, nd) if not inverse else \
+        bits.reshape(H, nw * 64 // (32 * nd), nd, 32)
+    out = g.transpose(0, 1, 3, 2).reshape(H, nw * 64)
+    return np.packbits(out, axis=1, bitorder="little").view(np.uint64)
+
+
+def test_il_layout_roundtrip():
+    rng = np.random.default_rng(1)
+    w = rng.integers(0, 2**63, size=(3, 8), dtype=np.uint64)
+    for nd in (2, 4):
+        assert np.array_equal(il_layout(il_layout(w, nd), nd, inverse=True), w)
+        assert not np.array_equal(il_layout(w, nd), w)
+
+
+@pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 8])
+@pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 19), (384, 3, 8, 11), (8320, 41, 7, 13),
+                                            (16384, 70, 64, 9), (2048, 300, 137, 17)])
+def test_temporal_blocking_interleaved(gol, oracle, monkeypatch, tpl, w, h, band, turns):
+    """The shipped temporal-blocking kernel (k_step_skew<IL>) runs on the interleaved word
+    layout; the engine converts on the way in and out and between multi-turn launches and
+    the k = 1 tail turns (turns not a multiple of tpl).  Bit-exact against the oracle, and
+    the board is the same when read mid-run and then stepped on."""
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "6")
+    start = oracle.gen_random(tpl * 7 + w, w, h)
+    with _engine(gol, w, h, band_rows=band, turns_per_launch=tpl) as e:
+        e.load_packed(start)
+        e.step(turns)
+        mid = e.read_packed()
+        t, alive = e.snapshot()
+        e.step(turns + 1)
+        got = e.read_packed()
+    want_mid = oracle.bit_run(start, w, turns)
+    assert np.array_equal(mid, want_mid)
+    assert (t, alive) == (turns, oracle.popcount(want_mid, w))
+    assert np.array_equal(got, oracle.bit_run(want_mid, w, turns + 1))
+
+
+def test_interleaved_raw_layout(gol, oracle, monkeypatch):
+    """What the IL kernel computes on: a board whose words are il_layout() of the logical
+    board.  Checked through a strip engine's halo export (standard rows) and the engine's
+    own conversion, against the numpy restatement of the layout."""
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "6")
+    torch = pytest.importorskip("torch")
+    w, rows, K = 512, 40, 8
+    start = oracle.gen_random(5, w, rows + 2 * K)
+    with gol.Engine(w, rows + 2 * K, device=0, row_offset=0, rows=rows, halo=K,
+                    turns_per_launch=4) as e:
+        e.load_packed(start)
+        e.step(4)                                   # now interleaved on the device
+        top = torch.zeros((K, w // 64), dtype=torch.int64, device="cuda")
+        bot = torch.zeros_like(top)
+        e.export_halo(top.data_ptr(), bot.data_ptr())
+        e.sync()
+        got = e.read_packed()
+    assert np.array_equal(top.cpu().numpy().view(np.uint64), got[:K])
+    assert np.array_equal(bot.cpu().numpy().view(np.uint64), got[rows - K:])
 
 
 @pytest.mark.parametrize("n,K,tpl", [(2, 8, 4), (3, 5, 4), (4, 6, 8), (1, 7, 3)])

@@ -43,7 +43,7 @@ def main():
                         e = gol.Engine(W, H, device=0, band_rows=b, turns_per_launch=k)
                         e.set_stream(stream.cuda_stream)
                         e.fill_random(3)
-                        e.step(5)
+                        e.step(2 * k)
                         engines[(v, e.info().band_rows, k, mw, mv)] = e
     torch.cuda.synchronize()
     res = {k: [] for k in engines}
