@@ -174,6 +174,27 @@ void autotune_multi(gol_ctx *c, bool tune_k)
     if (words < (1ll << 20)) return;                 // < 64 Mi cells: keep the defaults
     static const int kKs[] = {6, 8};
     static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
+    // plus the bands whose grid just fits 1..4 rounds of resident wavefronts (65536^2 at 4
+    // waves/SIMD: 274 -> 4080 of 4096 waves, 137 -> 8160 of 8192)
+    std::vector<int> bands(std::begin(kBands), std::end(kBands));
+    {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
+        const long long ntx = golk::multi_tiles(c->cfg.width, lane_dw);
+        for (int K : {6, 8}) {
+            const long long cap =
+                (long long)ncu * 4 * golk::multi_blocks_per_cu(K, c->multi_words, c->multi_variant);
+            for (int r = 1; r <= 4 && cap > 0; ++r) {
+                const long long nb = r * cap / ntx;
+                if (nb <= 0) continue;
+                const long long b = (c->cfg.rows + nb - 1) / nb;
+                if (b >= 16 && b <= 1024 && b <= c->cfg.rows) bands.push_back((int)b);
+            }
+        }
+        std::sort(bands.begin(), bands.end());
+        bands.erase(std::unique(bands.begin(), bands.end()), bands.end());
+    }
     golk::StepArgs a{};
     a.width = c->cfg.width;
     a.nw = c->nw;
@@ -199,14 +220,14 @@ void autotune_multi(gol_ctx *c, bool tune_k)
     else ks.push_back(c->tpl);
     for (int K : ks) {
         if (!golk::multi_ok(c->cfg.width, K)) continue;
-        for (int band : kBands) {
-            if (band > c->cfg.rows && band != kBands[0]) break;
+        for (int band : bands) {
+            if (band > c->cfg.rows && band != bands[0]) break;
             a.band = band;
             a.in = c->board[0];
             a.out = c->board[1];
             bool ok = golk::launch_step_multi(a, K, c->stream) == hipSuccess;   // warm
             ok = ok && hipEventRecord(e0, c->stream) == hipSuccess;
-            for (int rep = 0; rep < 2 && ok; ++rep) {
+            for (int rep = 0; rep < 4 && ok; ++rep) {
                 a.in = c->board[(rep + 1) & 1];
                 a.out = c->board[rep & 1];
                 ok = golk::launch_step_multi(a, K, c->stream) == hipSuccess;
@@ -215,7 +236,7 @@ void autotune_multi(gol_ctx *c, bool tune_k)
                  hipEventSynchronize(e1) == hipSuccess;
             float ms = 0.f;
             if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) continue;
-            const float per_turn = ms / (2.f * K);
+            const float per_turn = ms / (4.f * K);
             if (best == 0.f || per_turn < best) {
                 best = per_turn;
                 best_k = K;

@@ -69,6 +69,8 @@ hipError_t launch_il_convert(const uint64_t *in, int in_pitch, uint64_t *out, in
                              int nrows, int nw, bool to_il, hipStream_t s);
 // dwords per lane of the temporal-blocking kernel (tiles advance by 62 x that many dwords)
 int multi_lane_dwords(int words_per_lane, int variant);
+// wavefront tiles per row band of the temporal-blocking kernel
+long long multi_tiles(int width, int lane_dwords);
 int auto_band_multi(int width, int rows, int lane_dwords);
 // resident 256-thread blocks per CU of the temporal-blocking kernel (0 on error)
 int multi_blocks_per_cu(int turns, int words_per_lane, int variant);

@@ -1157,7 +1157,7 @@ int multi_lane_dwords(int words_per_lane, int variant)
     return variant == kMultiSkewD1 ? 1 : 2 * words_per_lane;
 }
 
-static inline long long multi_tiles(int width, int lane_dwords)
+long long multi_tiles(int width, int lane_dwords)
 {
     const long long nd = 2ll * ((width + 63) / 64);
     return (nd + 62 * lane_dwords - 1) / (62 * lane_dwords);
