@@ -61,7 +61,7 @@ bool fast_path_ok(int width);
 // no counts.  turns in {2, 3, 4, 5, 6, 8}.
 constexpr int kMaxTurnsPerLaunch = 8;
 bool multi_ok(int width, int turns);
-bool multi_fits(int nw, int pitch, int rows);   // buffer addressable with 32-bit dword offsets
+bool multi_fits(int nw, int pitch, int rows);   // buffer < 2 GiB (k_step_skew buffer ranges)
 // the temporal-blocking kernel for (words per lane, variant) runs on the interleaved layout
 bool multi_is_il(int words_per_lane, int variant);
 // standard <-> interleaved rows (row pitches in words; in and out may not alias)

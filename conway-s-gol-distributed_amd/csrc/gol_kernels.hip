@@ -604,6 +604,27 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
 // steady part is a multiple of U; rows past r_end feed only outputs >= y1 (not stored).
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 
+constexpr int kBufFlags = 0x00020000;                  // raw buffer, dword3 (CDNA)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void buf_store(const uint32_t (&o)[1], __amdgpu_buffer_rsrc_t r,
+                                          uint32_t voff, uint32_t soff)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(o[0], r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_store(const uint32_t (&o)[2], __amdgpu_buffer_rsrc_t r,
+                                          uint32_t voff, uint32_t soff)
+{
+    const u32x2 d = {o[0], o[1]};
+    __builtin_amdgcn_raw_buffer_store_b64(d, r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_store(const uint32_t (&o)[4], __amdgpu_buffer_rsrc_t r,
+                                          uint32_t voff, uint32_t soff)
+{
+    const u32x4 d = {o[0], o[1], o[2], o[3]};
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, soff, 0);
+}
+
 template <int ND> struct LaneDw;
 template <> struct LaneDw<1> { using T = uint32_t; };
 template <> struct LaneDw<2> { using T = uint2; };
@@ -618,7 +639,11 @@ __device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[
 // and dword ND-1's east need a 1-bit funnel shift (v_alignbit, half-rate on gfx950 like
 // DPP: tools/calib/valu_issue.hip), i.e. 2 instead of 2 * ND shifts per lane-row.
 // (ND == 1 makes both layouts the same.)
-template <int K, int ND, int PD, int MINW, bool R7, bool IL = false>
+// BUF: row loads (LDS-DMA) and stores through buffer resources -- per-lane byte offset in
+// one VGPR, the row (+ dword) offset in an SGPR (soffset): no
+// 64-bit VALU address adds, ~5 VGPRs freed; the halo lanes' stores are dropped by the
+// hardware range check (offset 2^31 >= num_records; buffers < 2 GiB, multi_fits).
+template <int K, int ND, int PD, int MINW, bool R7, bool IL = false, bool BUF = false>
 __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, StepArgs a,
                                                    int ntx)
@@ -664,16 +689,30 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
     };
     const char *inb = reinterpret_cast<const char *>(in);
     char *outb = reinterpret_cast<char *>(out);
+    const __amdgpu_buffer_rsrc_t rin =
+        __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)span, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rout =
+        __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)span, kBufFlags);
+    const uint32_t vst = st ? lane_b : 0x80000000u;     // halo lanes: out of range, dropped
     // prefetch ring in LDS: each wavefront owns RQ row slots of 64 lanes x ND dwords,
     // filled by LDS-DMA (global_load_lds_dword, dword k of every lane into plane k)
     __shared__ uint32_t lds_rows[4][RQ][ND][64];
     uint32_t(*slots)[ND][64] = lds_rows[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
     auto issue = [&](uint32_t off, auto Qc) {
         constexpr int q = decltype(Qc)::value;
-        const uint32_t *g = reinterpret_cast<const uint32_t *>((inb + off) + lane_b);
+        if constexpr (BUF) {
+            unroll_seq(std::make_integer_sequence<int, ND>{}, [&](auto Kc) {
+                constexpr int k = decltype(Kc)::value;
+                // (the immediate offset would move the LDS destination too: use soffset)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void *)&slots[q][k][0], 4,
+                                                         lane_b, off + 4 * k, 0, 0);
+            });
+        } else {
+            const uint32_t *g = reinterpret_cast<const uint32_t *>((inb + off) + lane_b);
 #pragma unroll
-        for (int k = 0; k < ND; ++k)
-            __builtin_amdgcn_global_load_lds(g + k, (lds_void *)&slots[q][k][0], 4, 0, 0);
+            for (int k = 0; k < ND; ++k)
+                __builtin_amdgcn_global_load_lds(g + k, (lds_void *)&slots[q][k][0], 4, 0, 0);
+        }
     };
     // row in slot q: wait until at most ND*(PD-1) vector-memory ops are outstanding -- the
     // ND*(PD-1) DMA dwords of the PD-1 later rows were issued after it (stores, when
@@ -762,8 +801,11 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
                 uint32_t o[ND];
                 stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, o);
                 if constexpr (RULE::value) {
-                    if (st && ry >= y0 && ry < y1)
+                    if constexpr (BUF) {
+                        if (ry >= y0 && ry < y1) buf_store(o, rout, vst, st_off);
+                    } else if (st && ry >= y0 && ry < y1) {
                         *reinterpret_cast<Vec *>((outb + st_off) + lane_b) = vec_make(o);
+                    }
                 }
             } else {
                 stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, XS[j + 1]);
@@ -1181,7 +1223,7 @@ bool multi_ok(int width, int turns)
 bool multi_fits(int nw, int pitch, int rows)
 {
     (void)nw;
-    return (long long)rows * pitch * 8 < (1ll << 32);   // 32-bit byte offsets in k_step_skew
+    return (long long)rows * pitch * 8 < (1ll << 31);   // k_step_skew buffer ranges < 2 GiB
 }
 
 // skew-kernel configurations (kMulti* variants): rows in flight, min waves per SIMD
@@ -1215,12 +1257,13 @@ template <int K, int ND> struct SkewCfg<kMultiSkewIL, K, ND> {
     static constexpr bool R7 = true;
 };
 
+
 template <int K, int ND, int Var>
 static void *skew_fn()
 {
     using C = SkewCfg<Var, K, ND>;
     return reinterpret_cast<void *>(
-        &k_step_skew<K, ND, C::PD, C::MINW, C::R7, Var == kMultiSkewIL>);
+        &k_step_skew<K, ND, C::PD, C::MINW, C::R7, Var == kMultiSkewIL, Var == kMultiSkewIL>);
 }
 
 // kernel for (turns, words per lane, variant); experimental variants exist for V = 1 and
