@@ -36,6 +36,14 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "cell updates/sec (GCUPS) at 16384² & 65536², 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_CELL_UPDATE = 0.25   # 1 bit read + 1 bit written per cell per turn
+# VALU-issue roofline of the temporal-blocking kernel (k_step_skew on the interleaved
+# layout): one stage-row of one wavefront (64 lanes x 64 cells = 4096 cell-updates) issues
+# 18 v_bitop3 (full rate: 2 SIMD cycles per wave64 instruction) + 2 v_alignbit + 2 DPP
+# moves (half rate: 4 cycles) = 52 SIMD cycles (rates: tools/calib/valu_issue.hip on
+# MI355X).  1024 SIMDs at the 2.4 GHz peak clock -> 193.6 T cell-updates/s per GPU, before
+# any redundant halo/pipeline work.
+VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES_PER_4096 = 1024, 2.4e9, 52.0
+VALU_PEAK_GCUPS = VALU_SIMDS * VALU_CLOCK_HZ / VALU_CYCLES_PER_4096 * 4096 / 1e9
 
 
 def parse():
@@ -191,8 +199,17 @@ def main():
                          # the same GCUPS priced at the k=1 definition (0.25 B per cell-update)
                          "k1_equivalent_frac": round(gcups / world * BYTES_PER_CELL_UPDATE
                                                      / HBM_PEAK_GBS, 4)},
+            "valu_roofline": None,
             "cpu_baseline": None,
         }
+        if K > 1:
+            per_gpu = gcups / world
+            out["valu_roofline"] = {
+                "bound": "valu", "achieved": round(per_gpu, 1), "peak": round(VALU_PEAK_GCUPS, 1),
+                "unit": "GCUPS per GPU", "frac": round(per_gpu / VALU_PEAK_GCUPS, 4),
+                "model": "52 SIMD cycles per 4096 cell-updates (18 full-rate v_bitop3 + 4 "
+                         "half-rate v_alignbit/DPP), 1024 SIMDs x 2.4 GHz; useful cell-updates "
+                         "only (halo lanes, band halos and pipeline fill count against it)"}
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(W, a.seed, a.cpu_turns, a.cpu_cores)
         print(json.dumps(out), flush=True)
