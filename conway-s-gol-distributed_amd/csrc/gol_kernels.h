@@ -39,6 +39,7 @@ enum : int {
     kMultiSkewD1 = 5,       // k_step_skew, 1 dword (32 cells) per lane     (V = 1, K = 4/6/8 only)
     kMultiSkewIL = 6,       // k_step_skew on the interleaved board layout (V = 1; the default)
     kMultiCount = 7,
+    kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 
 // fast-path stencil variants (A/B-able in one process; kVariantDefault is shipped)

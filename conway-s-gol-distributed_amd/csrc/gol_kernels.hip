@@ -643,7 +643,10 @@ __device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[
 // one VGPR, the row (+ dword) offset in an SGPR (soffset): no
 // 64-bit VALU address adds, ~5 VGPRs freed; the halo lanes' stores are dropped by the
 // hardware range check (offset 2^31 >= num_records; buffers < 2 GiB, multi_fits).
-template <int K, int ND, int PD, int MINW, bool R7, bool IL = false, bool BUF = false>
+// ABL: timing ablations (tools only, wrong results): 1 = no row DMA, 2 = no LDS read-back
+// (and no DMA wait), 4 = no output stores (kept live behind a runtime-false branch).
+template <int K, int ND, int PD, int MINW, bool R7, bool IL = false, bool BUF = false,
+          int ABL = 0>
 __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, StepArgs a,
                                                    int ntx)
@@ -700,6 +703,7 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
     uint32_t(*slots)[ND][64] = lds_rows[__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))];
     auto issue = [&](uint32_t off, auto Qc) {
         constexpr int q = decltype(Qc)::value;
+        if constexpr ((ABL & 1) != 0) return;
         if constexpr (BUF) {
             unroll_seq(std::make_integer_sequence<int, ND>{}, [&](auto Kc) {
                 constexpr int k = decltype(Kc)::value;
@@ -720,6 +724,11 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
     auto fetch = [&](auto Qc, uint32_t (&c)[ND]) {
         constexpr int q = decltype(Qc)::value;
         constexpr int n = ND * (PD - 1);
+        if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) c[k] = lane_b * (q + k + 1);
+            return;
+        }
         __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
 #pragma unroll
         for (int k = 0; k < ND; ++k) c[k] = slots[q][k][lane];
@@ -801,7 +810,9 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
                 uint32_t o[ND];
                 stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, o);
                 if constexpr (RULE::value) {
-                    if constexpr (BUF) {
+                    if constexpr ((ABL & 4) != 0) {
+                        if (a.cnt_hi == 0x7fffffff) buf_store(o, rout, vst, st_off);
+                    } else if constexpr (BUF) {
                         if (ry >= y0 && ry < y1) buf_store(o, rout, vst, st_off);
                     } else if (st && ry >= y0 && ry < y1) {
                         *reinterpret_cast<Vec *>((outb + st_off) + lane_b) = vec_make(o);
@@ -1191,7 +1202,7 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
 
 bool multi_is_il(int words_per_lane, int variant)
 {
-    return variant == kMultiSkewIL && words_per_lane == 1;
+    return (variant == kMultiSkewIL || variant >= kMultiAblate) && words_per_lane == 1;
 }
 
 int multi_lane_dwords(int words_per_lane, int variant)
@@ -1258,6 +1269,12 @@ template <int K, int ND> struct SkewCfg<kMultiSkewIL, K, ND> {
 };
 
 
+template <int ABL>
+static void *abl_fn()
+{
+    return reinterpret_cast<void *>(&k_step_skew<8, 2, 8, 4, true, true, true, ABL>);
+}
+
 template <int K, int ND, int Var>
 static void *skew_fn()
 {
@@ -1279,6 +1296,16 @@ static void *multi_fn(int turns, int variant)
         case 5: return reinterpret_cast<void *>(&k_step_multi<5, V>);
         case 6: return reinterpret_cast<void *>(&k_step_multi<6, V>);
         case 8: return reinterpret_cast<void *>(&k_step_multi<8, V>);
+        default: return nullptr;
+        }
+    }
+    if (V == 1 && turns == 8 && variant >= kMultiAblate) {   // timing ablations (tools only)
+        switch (variant - kMultiAblate) {
+        case 1: return abl_fn<1>();
+        case 2: return abl_fn<2>();
+        case 3: return abl_fn<3>();
+        case 4: return abl_fn<4>();
+        case 7: return abl_fn<7>();
         default: return nullptr;
         }
     }

@@ -1,7 +1,4 @@
-# round-1 profiles of the shipped default: kernel trace + stats, FETCH/WRITE, SQ counters
+# per-step overhead ablations of the K=8 IL kernel (wrong results; timing only)
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-bash tools/profile.sh || exit 1
-TAG=_k8il bash tools/pmc_sq.sh || exit 1
-python tools/pmc_report.py gpurun_out/pmc_sq_k8il/run_counter_collection.csv > gpurun_out/pmc_sq_k8il/report.txt
-cat gpurun_out/pmc_sq_k8il/report.txt
-tail -1 gpurun_out/prof/kt.log
+t() { timeout -k 10 300 "$@" 2>&1 | grep -v amdgpu.ids; }
+for v in 6 101 102 103 104 107 6; do echo "== variant $v"; GOL_MULTI_VARIANT=$v t python -u tools/occupancy_probe.py --waves 4 --band 256; done
