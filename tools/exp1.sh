@@ -1,4 +1,5 @@
-# per-step overhead ablations of the K=8 IL kernel (wrong results; timing only)
+# full GPU suite + smoke + default bench (with CPU baseline)
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-t() { timeout -k 10 300 "$@" 2>&1 | grep -v amdgpu.ids; }
-for v in 6 101 102 103 104 107 6; do echo "== variant $v"; GOL_MULTI_VARIANT=$v t python -u tools/occupancy_probe.py --waves 4 --band 256; done
+timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests > gpurun_out/t_all.log 2>&1; rc=$?; tail -3 gpurun_out/t_all.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_full.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/bench_full.log | tail -1; exit $rc
