@@ -641,8 +641,9 @@ __device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[
 // (ND == 1 makes both layouts the same.)
 // BUF: row loads (LDS-DMA) and stores through buffer resources -- per-lane byte offset in
 // one VGPR, the row (+ dword) offset in an SGPR (soffset): no
-// 64-bit VALU address adds, ~5 VGPRs freed; the halo lanes' stores are dropped by the
-// hardware range check (offset 2^31 >= num_records; buffers < 2 GiB, multi_fits).
+// 64-bit VALU address adds, ~5 VGPRs freed (num_records = the buffer size: < 2 GiB,
+// multi_fits).  Halo lanes skip their stores by exec mask (2 % faster than dropping them
+// with an out-of-range offset).
 // ABL: timing ablations (tools only, wrong results): 1 = no row DMA, 2 = no LDS read-back
 // (and no DMA wait), 4 = no output stores (kept live behind a runtime-false branch).
 template <int K, int ND, int PD, int MINW, bool R7, bool IL = false, bool BUF = false,
@@ -696,7 +697,6 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
         __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)span, kBufFlags);
     const __amdgpu_buffer_rsrc_t rout =
         __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)span, kBufFlags);
-    const uint32_t vst = st ? lane_b : 0x80000000u;     // halo lanes: out of range, dropped
     // prefetch ring in LDS: each wavefront owns RQ row slots of 64 lanes x ND dwords,
     // filled by LDS-DMA (global_load_lds_dword, dword k of every lane into plane k)
     __shared__ uint32_t lds_rows[4][RQ][ND][64];
@@ -811,9 +811,9 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
                 stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, o);
                 if constexpr (RULE::value) {
                     if constexpr ((ABL & 4) != 0) {
-                        if (a.cnt_hi == 0x7fffffff) buf_store(o, rout, vst, st_off);
+                        if (a.cnt_hi == 0x7fffffff) buf_store(o, rout, lane_b, st_off);
                     } else if constexpr (BUF) {
-                        if (ry >= y0 && ry < y1) buf_store(o, rout, vst, st_off);
+                        if (st && ry >= y0 && ry < y1) buf_store(o, rout, lane_b, st_off);
                     } else if (st && ry >= y0 && ry < y1) {
                         *reinterpret_cast<Vec *>((outb + st_off) + lane_b) = vec_make(o);
                     }
