@@ -23,6 +23,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -59,39 +60,94 @@ struct Item {
     std::shared_ptr<std::vector<int64_t>> cells;   // FinalTurnComplete.Alive
 };
 
+// Host image bytes in page-locked memory (hipHostMalloc), so PGM payloads move to and
+// from the device by DMA (hipMemcpyAsync without a pageable bounce); plain malloc if the
+// pinning fails.  The reference's io goroutine moves the image byte by byte over a
+// channel (Local/gol/io.go:88-121, 42-85).
+struct HostBuf {
+    uint8_t *p = nullptr;
+    size_t n = 0;
+    bool pinned = false;
+    HostBuf() = default;
+    HostBuf(const HostBuf &) = delete;
+    HostBuf &operator=(const HostBuf &) = delete;
+    HostBuf(HostBuf &&o) noexcept : p(o.p), n(o.n), pinned(o.pinned) { o.p = nullptr; o.n = 0; }
+    HostBuf &operator=(HostBuf &&o) noexcept
+    {
+        if (this != &o) {
+            release();
+            p = o.p;
+            n = o.n;
+            pinned = o.pinned;
+            o.p = nullptr;
+            o.n = 0;
+        }
+        return *this;
+    }
+    ~HostBuf() { release(); }
+    bool alloc(size_t bytes)
+    {
+        if (p && n == bytes) return true;
+        release();
+        if (bytes == 0) return true;
+        if (hipHostMalloc((void **)&p, bytes, hipHostMallocDefault) == hipSuccess) {
+            pinned = true;
+        } else {
+            (void)hipGetLastError();
+            p = (uint8_t *)std::malloc(bytes);
+            pinned = false;
+            if (!p) return false;
+        }
+        n = bytes;
+        return true;
+    }
+    void release()
+    {
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else std::free(p);
+        }
+        p = nullptr;
+        n = 0;
+    }
+    uint8_t *data() { return p; }
+    const uint8_t *data() const { return p; }
+    size_t size() const { return n; }
+};
+
 bool is_space(unsigned char ch) { return ch == ' ' || (ch >= '\t' && ch <= '\r'); }
 
 // strings.Fields-like split of the first 5 fields (Local/gol/io.go:93-114):
-// fields[4] is the payload, which ends at the next whitespace byte.
-int parse_pgm(const std::vector<uint8_t> &data, int W, int H, std::vector<uint8_t> &pix,
-              std::string &err)
+// fields[4] is the payload, which ends at the next whitespace byte.  On success
+// `payload` is the payload's offset in `data` (W*H bytes).
+int parse_pgm(const uint8_t *data, size_t size, int W, int H, size_t &payload, std::string &err)
 {
     size_t pos = 0;
     std::string f[4];
     for (int k = 0; k < 4; k++) {
-        while (pos < data.size() && is_space(data[pos])) pos++;
+        while (pos < size && is_space(data[pos])) pos++;
         size_t s = pos;
-        while (pos < data.size() && !is_space(data[pos])) pos++;
-        f[k].assign(data.begin() + (long)s, data.begin() + (long)pos);
+        while (pos < size && !is_space(data[pos])) pos++;
+        f[k].assign((const char *)data + s, pos - s);
     }
     if (f[0] != "P5") { err = "Not a pgm file"; return GOL_EIO; }
     if (atoi(f[1].c_str()) != W) { err = "Incorrect width"; return GOL_EIO; }
     if (atoi(f[2].c_str()) != H) { err = "Incorrect height"; return GOL_EIO; }
     if (atoi(f[3].c_str()) != 255) { err = "Incorrect maxval/bit depth"; return GOL_EIO; }
-    while (pos < data.size() && is_space(data[pos])) pos++;
+    while (pos < size && is_space(data[pos])) pos++;
     size_t s = pos;
-    while (pos < data.size() && !is_space(data[pos])) pos++;
+    while (pos < size && !is_space(data[pos])) pos++;
     const size_t need = (size_t)W * H;
     if (pos - s < need) {
         err = "PGM payload shorter than width*height (the reference would block on inputQ)";
         return GOL_EIO;
     }
-    pix.assign(data.begin() + (long)s, data.begin() + (long)(s + need));
+    payload = s;
     return GOL_OK;
 }
 
 int write_pgm(const std::string &dir, const std::string &name, int W, int H,
-              const std::vector<uint8_t> &pix, std::string &err)
+              const HostBuf &pix, std::string &err)
 {
     ::mkdir(dir.c_str(), 0777);                   // os.Mkdir("out", ...) (io.go:46)
     const std::string path = dir + "/" + name + ".pgm";
@@ -229,19 +285,23 @@ struct Strips {
         return GOL_OK;
     }
 
-    int load(const std::vector<uint8_t> &pix)
+    int load(const uint8_t *pix)
     {
         if (!strip_mode()) {
-            int rc = gol_load(eng[0], pix.data());
+            int rc = gol_load(eng[0], pix);
             return rc ? fail_from(eng[0], rc) : GOL_OK;
         }
+        HostBuf buf;
         for (size_t i = 0; i < eng.size(); i++) {
             const int br = rows[i] + 2 * K;
-            std::vector<uint8_t> buf((size_t)br * W);
+            if (!buf.alloc((size_t)br * W)) {
+                err = "out of host memory";
+                return GOL_ENOMEM;
+            }
             for (int b = 0; b < br; b++) {
                 int g = (off[i] - K + b) % H;
                 if (g < 0) g += H;
-                std::memcpy(buf.data() + (size_t)b * W, pix.data() + (size_t)g * W, (size_t)W);
+                std::memcpy(buf.data() + (size_t)b * W, pix + (size_t)g * W, (size_t)W);
             }
             int rc = gol_load(eng[i], buf.data());
             if (rc) return fail_from(eng[i], rc);
@@ -351,9 +411,12 @@ struct Strips {
         return GOL_OK;
     }
 
-    int read_board(std::vector<uint8_t> &pix)
+    int read_board(HostBuf &pix)
     {
-        pix.assign((size_t)W * H, 0);
+        if (!pix.alloc((size_t)W * H)) {
+            err = "out of host memory";
+            return GOL_ENOMEM;
+        }
         for (size_t i = 0; i < eng.size(); i++) {
             const int o = strip_mode() ? off[i] : 0;
             int rc = gol_read_board(eng[i], pix.data() + (size_t)o * W);
@@ -396,19 +459,24 @@ void gol_run::run()
 
     // ioInput: read images/{W}x{H}.pgm (distributor.go:73-83, io.go:88-121)
     const std::string fname = std::to_string(W) + "x" + std::to_string(H);
-    std::vector<uint8_t> file, pix;
+    HostBuf file;                                     // the whole file, pinned
+    size_t payload = 0;
     {
-        FILE *f = fopen((image_dir + "/" + fname + ".pgm").c_str(), "rb");
-        if (!f) return die("cannot open " + image_dir + "/" + fname + ".pgm");
-        uint8_t buf[1 << 16];
-        size_t n;
-        while ((n = fread(buf, 1, sizeof buf, f)) > 0) file.insert(file.end(), buf, buf + n);
+        const std::string path = image_dir + "/" + fname + ".pgm";
+        FILE *f = fopen(path.c_str(), "rb");
+        if (!f) return die("cannot open " + path);
+        long sz = -1;
+        if (fseek(f, 0, SEEK_END) == 0) sz = ftell(f);
+        if (sz < 0 || fseek(f, 0, SEEK_SET) != 0 || !file.alloc((size_t)sz) ||
+            fread(file.data(), 1, (size_t)sz, f) != (size_t)sz) {
+            fclose(f);
+            return die("cannot read " + path);
+        }
         fclose(f);
         std::string err;
-        if (parse_pgm(file, W, H, pix, err)) return die(err);
-        file.clear();
-        file.shrink_to_fit();
+        if (parse_pgm(file.data(), file.size(), W, H, payload, err)) return die(err);
     }
+    const uint8_t *pix = file.data() + payload;
 
     Strips st;
     if (st.create(W, H, ngpus, devices, halo, engine_flags)) return die(st.err);
@@ -457,7 +525,7 @@ void gol_run::run()
         return send(e);
     };
     auto save_image = [&](long long t) -> bool {      // 's' and the final output
-        std::vector<uint8_t> out;
+        HostBuf out;
         if (st.read_board(out)) { die(st.err); return false; }
         const std::string name = fname + "x" + std::to_string(t);
         std::string err;
@@ -467,10 +535,13 @@ void gol_run::run()
         return send(e);
     };
 
-    std::vector<uint8_t> prev;                        // CellFlipped: previous board
-    if (emit_cell_flipped) prev = pix;
-    pix.clear();
-    pix.shrink_to_fit();
+    HostBuf prev;                                     // CellFlipped: previous board
+    if (emit_cell_flipped) {
+        if (!prev.alloc((size_t)W * H)) return die("out of host memory");
+        std::memcpy(prev.data(), pix, (size_t)W * H);
+    }
+    pix = nullptr;
+    file.release();
 
     long long chunk = 1;
     bool quit = false, killed = false;
@@ -511,18 +582,18 @@ void gol_run::run()
         const double ms =
             std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
         if (emit_cell_flipped) {
-            std::vector<uint8_t> cur;
+            HostBuf cur;
             if (st.read_board(cur)) return die(st.err);
             // with CellFlipped on, chunks are single turns so every flip is reported
             for (int y = 0; y < H; y++)
                 for (int x = 0; x < W; x++)
-                    if (cur[(size_t)y * W + x] != prev[(size_t)y * W + x]) {
+                    if (cur.data()[(size_t)y * W + x] != prev.data()[(size_t)y * W + x]) {
                         gol_event cf = make_ev(GOL_EV_CELL_FLIPPED, turn + 1);
                         cf.x = x;
                         cf.y = y;
                         if (!send(cf)) return close();
                     }
-            prev.swap(cur);
+            std::swap(prev, cur);
         }
         if (emit_turn_complete)
             for (long long t = 1; t <= n; t++)
