@@ -1200,9 +1200,11 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
     return hipGetLastError();
 }
 
+constexpr bool is_il_variant(int v) { return v == kMultiSkewIL; }
+
 bool multi_is_il(int words_per_lane, int variant)
 {
-    return (variant == kMultiSkewIL || variant >= kMultiAblate) && words_per_lane == 1;
+    return (is_il_variant(variant) || variant >= kMultiAblate) && words_per_lane == 1;
 }
 
 int multi_lane_dwords(int words_per_lane, int variant)
@@ -1269,6 +1271,7 @@ template <int K, int ND> struct SkewCfg<kMultiSkewIL, K, ND> {
 };
 
 
+
 template <int ABL>
 static void *abl_fn()
 {
@@ -1280,7 +1283,7 @@ static void *skew_fn()
 {
     using C = SkewCfg<Var, K, ND>;
     return reinterpret_cast<void *>(
-        &k_step_skew<K, ND, C::PD, C::MINW, C::R7, Var == kMultiSkewIL, Var == kMultiSkewIL>);
+        &k_step_skew<K, ND, C::PD, C::MINW, C::R7, is_il_variant(Var), is_il_variant(Var)>);
 }
 
 // kernel for (turns, words per lane, variant); experimental variants exist for V = 1 and
@@ -1356,7 +1359,7 @@ static hipError_t launch_multi_v(const StepArgs &a, int turns, hipStream_t s)
     int var = a.multi_variant;                          // depths D1 lacks: 2 dwords per lane
     if (var == kMultiSkewD1 && !(V == 1 && (turns == 4 || turns == 6 || turns == 8)))
         var = kMultiSkew;
-    if (var == kMultiSkewIL && V != 1) var = kMultiSkew; // multi_is_il() is false for V = 2
+    if (is_il_variant(var) && V != 1) var = kMultiSkew;  // multi_is_il() is false for V = 2
     const int ntx = (int)multi_tiles(a.width, multi_lane_dwords(V, var));
     const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
     const long long nwaves = (long long)ntx * nbands;
