@@ -12,8 +12,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o run --output-fo
   python3 "$R/bench.py" > "$O/kt.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline > "$O/fetch.log" 2>&1
+  python3 "$R/bench.py" --steps 200 --warmup 8 --no-cpu-baseline > "$O/fetch.log" 2>&1
 rc=$?; echo "fetch rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d "$O/write" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline > "$O/write.log" 2>&1
+  python3 "$R/bench.py" --steps 200 --warmup 8 --no-cpu-baseline > "$O/write.log" 2>&1
 rc=$?; echo "write rc=$rc"; exit $rc

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Summarise a tools/profile.sh run (gpurun_out/prof) into profiles/<tag>_*.{csv,json}.
 
-traffic per launch = (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 bytes for the stencil kernel:
+traffic per launch = (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 bytes for the stencil kernel,
+medians over the last 20 dispatches of the top kernel (the timed launches):
 FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads exactly half of a wide
-(16 B/lane) coalesced stream (MI355X_MICROARCH.md, HBM section), so it is doubled;
+(16 B/lane) coalesced stream (MI355X_MICROARCH.md, HBM section) and of the stencil's own
+4-B/lane LDS-DMA row stream (tools/calib/calib_fetch.hip: 0.501 GiB for 1 GiB), so it is
+doubled;
 WRITE_SIZE is exact for 16-B-per-lane stores.  Infinity-Cache hits are included in
 both, so this is fabric traffic out of the XCD L2s (an upper bound on HBM bytes)."""
 import csv
@@ -50,8 +53,12 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_step"):
         p = os.path.join(src, name, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
+        # the bench's timed launches are the last dispatches of the top kernel; the
+        # engine's create-time autotune dispatches the same kernel on other bands first
         rows = [r for r in csv.DictReader(open(p))
-                if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
+                if r["Kernel_Name"] == top["Name"] and r["Counter_Name"] == counter]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        rows = rows[-20:]
         res[counter + "_kib_median"] = statistics.median(float(r["Counter_Value"]) for r in rows)
         res[counter + "_launches"] = len(rows)
     if "FETCH_SIZE_kib_median" in res and "WRITE_SIZE_kib_median" in res:
