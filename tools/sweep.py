@@ -5,6 +5,7 @@ usage: python tools/sweep.py [--size 65536] [--turns 100] [--rounds 3] [--varian
        [--bands 0,16,32,64,128]"""
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -32,6 +33,8 @@ def main():
     W, H = a.size, a.height or a.size
     stream = torch.cuda.Stream()
     engines = {}
+    # warm-up turns: a multiple of every turns-per-launch, so all engines stay on one turn
+    warm = 2 * math.lcm(*[int(x) for x in a.tpl.split(",")])
     for v in [int(x) for x in a.variants.split(",")]:
         for b in [int(x) for x in a.bands.split(",")]:
             for k in [int(x) for x in a.tpl.split(",")]:
@@ -43,7 +46,7 @@ def main():
                         e = gol.Engine(W, H, device=0, band_rows=b, turns_per_launch=k)
                         e.set_stream(stream.cuda_stream)
                         e.fill_random(3)
-                        e.step(2 * k)
+                        e.step(warm)
                         engines[(v, e.info().band_rows, k, mw, mv)] = e
     torch.cuda.synchronize()
     res = {k: [] for k in engines}
