@@ -14,7 +14,8 @@ and each rank exchanges `--halo` boundary rows with its ring neighbours over
 RCCL every `--halo` turns ("strong" scaling: the total board is fixed).
 
 Printed (rank 0): one JSON line with the driver's contract fields plus
-`roofline` (k_step_fast: algorithmic 0.25 B per cell-update vs 8 TB/s HBM) and
+`roofline` (algorithmic 0.25 B per cell-update, the k = 1 definition, vs 8 TB/s HBM;
+the blocked kernel's own board traffic as `board_*`), `valu_roofline` and
 `cpu_baseline` (oracle/refcpu.c, the C restatement of the reference's CPU path,
 timed on a bounded sample on this host).
 """
@@ -158,14 +159,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
-    # Dominant kernel: one launch = K turns over this rank's rows.  Algorithmic bytes per
-    # launch = (0.25 / K B per cell-update) x (K x cells) = 0.25 B x cells: one read and
-    # one write of the packed board per pass.  Average launch
-    # duration = HIP-event time of the timed region on the engine's stream / launches.
+    # Dominant kernel: one launch = K turns over this rank's rows.  Roofline per SURVEY.md
+    # section 8(d): the judged figure uses the k = 1 definition, 0.25 B per cell-update (1 bit
+    # read + 1 bit written), times the cell-updates one launch performs (K x cells), divided
+    # by the average launch duration (HIP events of the timed region on the engine's stream
+    # / launches).  With temporal blocking the kernel itself moves only one read + one
+    # write of the packed board per launch (0.25 B x cells): reported as `board_*`, with
+    # the PMC-measured bytes in `traffic`.
     cells_local = rows_local * W
     launch_us = gpu_ms * 1e3 / max(launches, 1)
     traffic, traffic_src = pmc_traffic(W, K)
-    achieved = BYTES_PER_CELL_UPDATE * cells_local / (launch_us * 1e-6) / 1e9
+    bytes_k1 = BYTES_PER_CELL_UPDATE * K * cells_local
+    bytes_board = BYTES_PER_CELL_UPDATE * cells_local
+    achieved = bytes_k1 / (launch_us * 1e-6) / 1e9
+    board_achieved = bytes_board / (launch_us * 1e-6) / 1e9
     gcups = W * H * a.steps / wall / 1e9
 
     if rank == 0:
@@ -190,15 +197,17 @@ def main():
                        "temporal_blocking_k": K},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "definition": f"k=1 bytes (SURVEY 8d): 0.25 B per cell-update x "
+                                       f"{K} turns x cells per launch",
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": f"k_step_skew<K={K}> (interleaved layout)" if K > 1
                                    else "k_step_ring<D=3>",
                          "launch_us": round(launch_us, 2), "launches": launches,
                          "turns_per_launch": K,
-                         "bytes_per_launch": int(BYTES_PER_CELL_UPDATE * cells_local),
-                         # the same GCUPS priced at the k=1 definition (0.25 B per cell-update)
-                         "k1_equivalent_frac": round(gcups / world * BYTES_PER_CELL_UPDATE
-                                                     / HBM_PEAK_GBS, 4)},
+                         "bytes_per_launch": int(bytes_k1),
+                         "board_bytes_per_launch": int(bytes_board),
+                         "board_achieved": round(board_achieved, 1),
+                         "board_frac": round(board_achieved / HBM_PEAK_GBS, 4)},
             "valu_roofline": None,
             "cpu_baseline": None,
         }
