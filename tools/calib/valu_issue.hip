@@ -43,6 +43,31 @@ __global__ __launch_bounds__(256) void k_issue(unsigned long long *cyc, unsigned
             if constexpr (OP == 7) { OP8("v_and_or_b32 %0, %0, %1, %2") }
             if constexpr (OP == 8) { OP8("v_xor_b32_dpp %0, %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0") }
             if constexpr (OP == 9) { OP8("v_fma_f32 %0, %0, %1, %2") }
+            if constexpr (OP == 10) {   // one dependent chain (8 deep per OP8 group)
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+            }
+            if constexpr (OP == 11) {   // two interleaved dependent chains
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a1) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a1) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a1) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a0) : "v"(b), "v"(c));
+                asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a1) : "v"(b), "v"(c));
+            }
+            if constexpr (OP == 12) {   // the stencil's mix: 9 bitop3 : 1 alignbit : 1 DPP
+                OP8("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96")
+                asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(a0) : "v"(b));
+                asm volatile("v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:0" : "+v"(a1) : "v"(c));
+            }
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -58,7 +83,8 @@ __global__ __launch_bounds__(256) void k_issue(unsigned long long *cyc, unsigned
 
 static const char *kNames[] = {"v_bitop3_b32", "v_alignbit_b32", "v_mov_b32_dpp", "v_xor_b32",
                                "v_or3_b32", "v_lshl_or_b32", "v_add_u32", "v_and_or_b32",
-                               "v_xor_b32_dpp", "v_fma_f32"};
+                               "v_xor_b32_dpp", "v_fma_f32", "bitop3 chain x1", "bitop3 chains x2",
+                               "mix 8 bitop3+1 align+1 dpp"};
 
 template <int OP>
 static void run(int W, int iters, int ncu)
@@ -75,7 +101,8 @@ static void run(int W, int iters, int ncu)
     (void)hipMemcpy(h.data(), d_cyc, h.size() * 8, hipMemcpyDeviceToHost);
     std::vector<double> cpi, ghz;
     for (int w = 0; w < blocks * 4; ++w) {
-        cpi.push_back((double)h[2 * w] / ((double)W * iters * 32));
+        const double per_iter = OP == 12 ? 40.0 : 32.0;
+        cpi.push_back((double)h[2 * w] / ((double)W * iters * per_iter));
         ghz.push_back((double)h[2 * w] / (double)h[2 * w + 1] * 0.1);
     }
     std::sort(cpi.begin(), cpi.end());
@@ -109,5 +136,8 @@ int main(int argc, char **argv)
     sweep<7>(iters, ncu);
     sweep<8>(iters, ncu);
     sweep<9>(iters, ncu);
+    sweep<10>(iters, ncu);
+    sweep<11>(iters, ncu);
+    sweep<12>(iters, ncu);
     return 0;
 }
