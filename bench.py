@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-turns", type=int, default=2)
     ap.add_argument("--cpu-cores", type=int, default=16)
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="N > 1 transport: nccl (= RCCL over xGMI); gloo stages halos through "
+                         "host memory and lets ranks share a GPU (tests only)")
     return ap.parse_args()
 
 
@@ -101,10 +104,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local if a.backend == "nccl" else local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    dev_ids = [gpu] if a.backend == "nccl" else None
 
     import gol
     from gol.distributed import DistStrip, EngineStrip, make_engine_strip
@@ -114,16 +122,17 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     if world == 1:
-        eng = gol.Engine(W, H, device=local, band_rows=a.band, turns_per_launch=a.tpl)
+        eng = gol.Engine(W, H, device=gpu, band_rows=a.band, turns_per_launch=a.tpl)
         eng.set_stream(stream.cuda_stream)
         eng.fill_random(a.seed)
         runner = eng
         rows_local = H
     else:
-        eng = make_engine_strip(W, H, rank, world, a.halo, local, band_rows=a.band,
+        eng = make_engine_strip(W, H, rank, world, a.halo, gpu, band_rows=a.band,
                                 turns_per_launch=a.tpl)
         eng.fill_random(a.seed)
-        runner = DistStrip(EngineStrip(eng, dev, stream), rank, world)
+        runner = DistStrip(EngineStrip(eng, dev, stream), rank, world,
+                           stage_on_host=a.backend == "gloo")
         rows_local = eng.rows
     info = eng.info()
 
@@ -134,7 +143,7 @@ def main():
     runner.step(a.warmup)
     torch.cuda.synchronize(dev)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        dist.barrier(device_ids=dev_ids)
     torch.cuda.synchronize(dev)
 
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -146,7 +155,7 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        dist.barrier(device_ids=dev_ids)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
@@ -155,7 +164,8 @@ def main():
     K = info.turns_per_launch
 
     if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        t = torch.tensor([wall], dtype=torch.float64,
+                         device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
@@ -192,7 +202,9 @@ def main():
             "config": {"workload": f"{W}x{H} random torus board (seed {a.seed}), "
                                    f"{a.steps} turns, bit-packed stencil, {K} turns per launch",
                        "board": [W, H], "turns": a.steps,
-                       "parallelism": f"row-strips x{world}" + (f", halo {info.halo}" if world > 1 else ""),
+                       "parallelism": f"row-strips x{world}" + (
+                           f", halo {info.halo}, {'RCCL' if a.backend == 'nccl' else 'gloo host-staged'}"
+                           if world > 1 else ""),
                        "band_rows": info.band_rows, "fast_path": bool(info.fast_path),
                        "temporal_blocking_k": K},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
