@@ -47,7 +47,7 @@ struct gol_ctx {
     int variant = golk::kVariantDefault;
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
     int multi_words = 2;                     // k_step_multi words per lane
-    int multi_variant = golk::kMultiSkewIL;  // temporal-blocking kernel (kMulti*)
+    int multi_variant = golk::kMultiSkewILW16;  // temporal-blocking kernel (kMulti*)
     int band_multi = 64;                     // band height of the multi-turn kernel
     float tuned_us_per_turn = 0.f;           // autotune's best measurement (0 = not tuned)
     uint64_t *board[2] = {nullptr, nullptr};

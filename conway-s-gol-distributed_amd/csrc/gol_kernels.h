@@ -28,7 +28,7 @@ struct StepArgs {
     int multi_variant;                 // temporal-blocking kernel (kMulti*)
 };
 
-// temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkewIL is shipped)
+// temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkewILW16 is shipped)
 enum : int {
     kMultiSerial = 0,       // k_step_multi: stages chained within a step
     kMultiSkew = 1,         // k_step_skew: stages one step apart, LDS-DMA prefetch of 8 rows,
@@ -37,8 +37,9 @@ enum : int {
     kMultiSkewW1 = 3,       // k_step_skew, no wave floor                   (V = 1, K = 6/8 only)
     kMultiSkewRule8 = 4,    // k_step_skew with the 8-op rule               (V = 1, K = 6/8 only)
     kMultiSkewD1 = 5,       // k_step_skew, 1 dword (32 cells) per lane     (V = 1, K = 4/6/8 only)
-    kMultiSkewIL = 6,       // k_step_skew on the interleaved board layout (V = 1; the default)
-    kMultiCount = 7,
+    kMultiSkewIL = 6,       // k_step_skew on the interleaved board layout (V = 1)
+    kMultiSkewILW16 = 7,    // kMultiSkewIL, one 16-B row DMA from half the lanes (V = 1; default)
+    kMultiCount = 8,
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 

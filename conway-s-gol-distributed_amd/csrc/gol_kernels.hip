@@ -646,14 +646,19 @@ __device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[
 // with an out-of-range offset).
 // ABL: timing ablations (tools only, wrong results): 1 = no row DMA, 2 = no LDS read-back
 // (and no DMA wait), 4 = no output stores (kept live behind a runtime-false branch).
+// W16 (ND = 2, BUF): one 16-B LDS-DMA per row from lanes 0..31 (word pairs) instead of two
+// 4-B DMAs from all lanes.  Tiles start one word later (lane 0 holds an even word, so no
+// pair straddles the row's wrap; the last tile stores word 0), and the slot holds the row's
+// 64 words in order (read back as one ds_read_b64 per lane).
 template <int K, int ND, int PD, int MINW, bool R7, bool IL = false, bool BUF = false,
-          int ABL = 0>
+          int ABL = 0, bool W16 = false>
 __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, StepArgs a,
                                                    int ntx)
 {
     static_assert(K >= 2, "one turn per launch is k_step_ring");
     static_assert(K <= 32 * ND, "the edge error must stay inside the halo lanes");
+    static_assert(!W16 || (ND == 2 && BUF), "wide row DMA: 2 dwords per lane, buffer path");
     constexpr int STRIDE = 62 * ND;                     // stored dwords per tile
     constexpr int RQ = PD + 1;                          // prefetch ring slots
     constexpr int U = 3 * RQ / cgcd(3, RQ);             // steady-loop unroll
@@ -670,14 +675,21 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
     nr = S0_ + (nr - S0_ + U - 1) / U * U;
 
     const int nd = 2 * a.nw;                            // dwords per row
-    const int t0 = tx * STRIDE;
-    const int t1 = min(t0 + STRIDE, nd);
+    constexpr int SHIFT = W16 ? ND : 0;                 // W16: tiles start one word later
+    const int t0 = tx * STRIDE + SHIFT;
+    const int t1 = min(t0 + STRIDE, nd + SHIFT);
     const int last = (t1 - t0 + ND - 1) / ND + 1;       // right halo lane
     const bool st = lane >= 1 && lane < last;
     int w = t0 - ND + ND * lane;                        // lane's first dword (torus wrap)
     while (w < 0) w += nd;
     while (w >= nd) w -= nd;
     const uint32_t lane_b = (uint32_t)w * 4u;
+    uint32_t lane_dma = 0;                              // W16: word pair of lanes 2L, 2L+1
+    if constexpr (W16) {
+        int pw = t0 - ND + 4 * (lane & 31);
+        while (pw >= nd) pw -= nd;
+        lane_dma = (uint32_t)pw * 4u;
+    }
     // byte offsets fit 32 bits: the host launches this kernel only on buffers < 4 GiB
     const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
     const int M = a.modrows;
@@ -704,7 +716,11 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
     auto issue = [&](uint32_t off, auto Qc) {
         constexpr int q = decltype(Qc)::value;
         if constexpr ((ABL & 1) != 0) return;
-        if constexpr (BUF) {
+        if constexpr (W16) {
+            if (lane < 32)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void *)&slots[q][0][0], 16,
+                                                         lane_dma, off, 0, 0);
+        } else if constexpr (BUF) {
             unroll_seq(std::make_integer_sequence<int, ND>{}, [&](auto Kc) {
                 constexpr int k = decltype(Kc)::value;
                 // (the immediate offset would move the LDS destination too: use soffset)
@@ -723,15 +739,21 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
     // present, only make the wait earlier), then read it back
     auto fetch = [&](auto Qc, uint32_t (&c)[ND]) {
         constexpr int q = decltype(Qc)::value;
-        constexpr int n = ND * (PD - 1);
+        constexpr int n = (W16 ? 1 : ND) * (PD - 1);
         if constexpr ((ABL & 2) != 0) {
 #pragma unroll
             for (int k = 0; k < ND; ++k) c[k] = lane_b * (q + k + 1);
             return;
         }
         __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
+        if constexpr (W16) {
+            const uint32_t *sp = &slots[q][0][0] + 2 * lane;
+            c[0] = sp[0];
+            c[1] = sp[1];
+        } else {
 #pragma unroll
-        for (int k = 0; k < ND; ++k) c[k] = slots[q][k][lane];
+            for (int k = 0; k < ND; ++k) c[k] = slots[q][k][lane];
+        }
     };
 
     uint32_t S0[K][3][ND], S1[K][3][ND], X[K][3][ND], XS[K][ND];
@@ -1200,7 +1222,7 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
     return hipGetLastError();
 }
 
-constexpr bool is_il_variant(int v) { return v == kMultiSkewIL; }
+constexpr bool is_il_variant(int v) { return v == kMultiSkewIL || v == kMultiSkewILW16; }
 
 bool multi_is_il(int words_per_lane, int variant)
 {
@@ -1269,6 +1291,10 @@ template <int K, int ND> struct SkewCfg<kMultiSkewIL, K, ND> {
     static constexpr int PD = 8, MINW = 4;
     static constexpr bool R7 = true;
 };
+template <int K, int ND> struct SkewCfg<kMultiSkewILW16, K, ND> {
+    static constexpr int PD = 8, MINW = 4;
+    static constexpr bool R7 = true;
+};
 
 
 
@@ -1283,7 +1309,8 @@ static void *skew_fn()
 {
     using C = SkewCfg<Var, K, ND>;
     return reinterpret_cast<void *>(
-        &k_step_skew<K, ND, C::PD, C::MINW, C::R7, is_il_variant(Var), is_il_variant(Var)>);
+        &k_step_skew<K, ND, C::PD, C::MINW, C::R7, is_il_variant(Var), is_il_variant(Var), 0,
+                     Var == kMultiSkewILW16>);
 }
 
 // kernel for (turns, words per lane, variant); experimental variants exist for V = 1 and
@@ -1309,6 +1336,17 @@ static void *multi_fn(int turns, int variant)
         case 3: return abl_fn<3>();
         case 4: return abl_fn<4>();
         case 7: return abl_fn<7>();
+        default: return nullptr;
+        }
+    }
+    if (V == 1 && variant == kMultiSkewILW16) {
+        switch (turns) {
+        case 2: return skew_fn<2, 2, kMultiSkewILW16>();
+        case 3: return skew_fn<3, 2, kMultiSkewILW16>();
+        case 4: return skew_fn<4, 2, kMultiSkewILW16>();
+        case 5: return skew_fn<5, 2, kMultiSkewILW16>();
+        case 6: return skew_fn<6, 2, kMultiSkewILW16>();
+        case 8: return skew_fn<8, 2, kMultiSkewILW16>();
         default: return nullptr;
         }
     }

@@ -150,7 +150,7 @@ def test_temporal_blocking(gol, oracle, monkeypatch, mw, tpl, w, h, band, turns)
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("mv", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("mv", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("tpl", [6, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 17), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (512, 130, 1000, 24),
@@ -189,15 +189,17 @@ def test_il_layout_roundtrip():
         assert not np.array_equal(il_layout(w, nd), w)
 
 
+@pytest.mark.parametrize("mv", [6, 7])
 @pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 19), (384, 3, 8, 11), (8320, 41, 7, 13),
-                                            (16384, 70, 64, 9), (2048, 300, 137, 17)])
-def test_temporal_blocking_interleaved(gol, oracle, monkeypatch, tpl, w, h, band, turns):
+                                            (16384, 70, 64, 9), (2048, 300, 137, 17),
+                                            (8064, 33, 16, 8), (7936, 20, 9, 16)])
+def test_temporal_blocking_interleaved(gol, oracle, monkeypatch, mv, tpl, w, h, band, turns):
     """The shipped temporal-blocking kernel (k_step_skew<IL>) runs on the interleaved word
     layout; the engine converts on the way in and out and between multi-turn launches and
     the k = 1 tail turns (turns not a multiple of tpl).  Bit-exact against the oracle, and
     the board is the same when read mid-run and then stepped on."""
-    monkeypatch.setenv("GOL_MULTI_VARIANT", "6")
+    monkeypatch.setenv("GOL_MULTI_VARIANT", str(mv))
     start = oracle.gen_random(tpl * 7 + w, w, h)
     with _engine(gol, w, h, band_rows=band, turns_per_launch=tpl) as e:
         e.load_packed(start)
