@@ -117,7 +117,10 @@ int gol_load(gol_ctx *ctx, const uint8_t *bytes);
  * y the GLOBAL row (oracle/bitref.c uses the same definition).  Resets turn. */
 int gol_fill_random(gol_ctx *ctx, uint64_t seed);
 /* Load / read packed words for the buffer rows (strip: incl. halos), row stride
- * words_per_row, for checkers that work on packed boards. */
+ * words_per_row, for checkers that work on packed boards.  Packed words crossing
+ * the ABI (here, gol_read_packed and the halo rows of gol_export_halo /
+ * gol_import_halo) are always in the standard layout (cell x = bit x % 64 of word
+ * x / 64), whatever internal layout the temporal-blocking kernel runs on. */
 int gol_load_packed(gol_ctx *ctx, const uint64_t *words);
 
 /* Advance `turns` turns.  Torus engine: any turns >= 0.  Strip engine:
