@@ -214,3 +214,39 @@ def test_cont_resume(gol, workdir, oracle):
     assert list(events) == []
     h.wait(5)
     assert h.error and "CONT" in h.error
+
+
+def _write_random_pgm(workdir, oracle, seed, w, h):
+    board = oracle.unpack(oracle.gen_random(seed, w, h), w)
+    (workdir / "images" / f"{w}x{h}.pgm").write_bytes(f"P5\n{w} {h}\n255\n".encode() +
+                                                     board.tobytes())
+
+
+def _digest(key):
+    import json
+    here = os.path.dirname(os.path.abspath(__file__))
+    return json.load(open(os.path.join(here, "golden", "large_digests.json")))[key]
+
+
+@pytest.mark.parametrize("key,ngpus", [("5120x5120_seed1_t1000", 1),
+                                       ("16384x16384_seed2_t10000", 2)])
+def test_baseline_configs_through_run(gol, workdir, oracle, key, ngpus):
+    """BASELINE configs C2 (5120^2 PGM, 1000 turns, 1 GPU) and C3 (16384^2, 10000 turns,
+    2 strips) end to end through gol.Run: PGM in (pinned), turns, TurnComplete events,
+    FinalTurnComplete, PGM out -- against the oracle-computed digests."""
+    import hashlib
+    d = _digest(key)
+    w, h, turns = d["width"], d["height"], d["turns"]
+    _write_random_pgm(workdir, oracle, d["seed"], w, h)
+    p = gol.Params(Turns=turns, Threads=8, ImageWidth=w, ImageHeight=h)
+    kw = dict(ngpus=ngpus, devices=[0] * ngpus, halo=128) if ngpus > 1 else {}
+    evs = run_collect(gol, p, workdir, **kw)
+    final = [e for e in evs if isinstance(e, gol.FinalTurnComplete)]
+    assert len(final) == 1 and final[0].CompletedTurns == turns
+    assert len(final[0].Alive) == d["alive"]
+    tc = [e.CompletedTurns for e in evs if isinstance(e, gol.TurnComplete)]
+    assert tc == list(range(1, turns + 1))
+    out = (workdir / "out" / f"{w}x{h}x{turns}.pgm").read_bytes()
+    board = G.parse_pgm(out)
+    words, _, nb = oracle.pack(board)
+    assert nb == 0 and hashlib.sha256(words.tobytes()).hexdigest() == d["sha256"]
