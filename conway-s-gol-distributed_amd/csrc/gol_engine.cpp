@@ -907,6 +907,33 @@ int gol_halo_done(gol_ctx *c)
     return GOL_OK;
 }
 
+int gol_halo_buffers(gol_ctx *c, void **send_top, void **send_bottom, void **recv_top,
+                     void **recv_bottom, int32_t *layout)
+{
+    if (!c || !send_top || !send_bottom || !recv_top || !recv_bottom || !layout)
+        return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!is_strip(c)) return fail(c, GOL_ESTATE, "not a strip engine");
+    DeviceGuard g(c->device);
+    // the layout the first launch after a full exchange runs on (gol_step's rule at
+    // halo_valid == halo): a function of width, halo and flags only, so equal on every rank
+    bool il = false;
+    if (c->tpl > 1 && !(c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) && !c->blocked_pending) {
+        int k = std::min(c->cfg.halo, c->tpl);
+        if (k == 7) k = 6;
+        il = golk::multi_ok(c->cfg.width, k) && golk::multi_is_il(c->multi_words, c->multi_variant);
+    }
+    if (int rc = ensure_layout(c, il)) return rc;
+    uint64_t *b = c->board[c->cur];
+    const int K = c->cfg.halo;
+    *send_top = b + (size_t)own_lo(c) * c->pitch;
+    *send_bottom = b + (size_t)(own_hi(c) - K) * c->pitch;
+    *recv_top = b;
+    *recv_bottom = b + (size_t)own_hi(c) * c->pitch;
+    *layout = c->il ? 1 : 0;
+    return GOL_OK;
+}
+
 }  // extern "C"
 
 // ------------------------------------------------- internal (driver) access

@@ -118,6 +118,9 @@ SIGNATURES = {
     "gol_copy_halo_from_upper": (_i32, [_vp, _vp]),
     "gol_copy_halo_from_lower": (_i32, [_vp, _vp]),
     "gol_halo_done": (_i32, [_vp]),
+    "gol_halo_buffers": (_i32, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                ctypes.POINTER(ctypes.c_int32)]),
     "gol_run_start": (_i32, [ctypes.POINTER(gol_params), ctypes.POINTER(gol_run_options),
                              ctypes.POINTER(_vp)]),
     "gol_run_next_event": (_i32, [_vp, ctypes.POINTER(gol_event), _i32]),

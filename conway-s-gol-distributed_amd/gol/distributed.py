@@ -26,41 +26,85 @@ TAG_UP = 17      # rows travelling to the upper neighbour (they become its botto
 TAG_DOWN = 18    # rows travelling to the lower neighbour (they become its top halo)
 
 
+class _DeviceRows:
+    """``__cuda_array_interface__`` view of ``shape`` int64 words at a device pointer the
+    engine owns (torch.as_tensor wraps it without a copy)."""
+
+    def __init__(self, ptr: int, shape):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": "<i8",
+                                         "data": (int(ptr), False), "version": 2,
+                                         "strides": None}
+
+
 class EngineStrip:
     """Adapter exposing an Engine strip to the exchange loop with torch tensors.
 
     The engine and the halo messages share one dedicated torch stream, so the RCCL
     send/recv that torch enqueues are ordered after the engine's turns and before its
-    next ones without host synchronisation."""
+    next ones without host synchronisation.
 
-    def __init__(self, engine: Engine, device: torch.device, stream=None):
+    ``zero_copy`` (default): the messages are views of the engine's own board rows
+    (``gol_halo_buffers``) -- RCCL reads the boundary rows and writes the halo rows in
+    place, in the engine's stepping layout, so an exchange launches nothing but the
+    transport.  Otherwise the rows are copied through separate buffers in the standard
+    layout (``gol_export_halo`` / ``gol_import_halo``)."""
+
+    def __init__(self, engine: Engine, device: torch.device, stream=None,
+                 zero_copy: bool = True):
         self.engine = engine
         self.device = device
         self.stream = stream if stream is not None else torch.cuda.Stream(device)
         engine.set_stream(self.stream.cuda_stream)
+        self.zero_copy = bool(zero_copy)
+        self.layout = None
+        self._views = None
         K, nw = engine.halo, engine.words_per_row
-        mk = lambda: torch.empty((K, nw), dtype=torch.int64, device=device)  # noqa: E731
-        self.top_send, self.bot_send, self.top_recv, self.bot_recv = mk(), mk(), mk(), mk()
+        self._shape = (K, nw)
+        if not self.zero_copy:
+            mk = lambda: torch.empty((K, nw), dtype=torch.int64, device=device)  # noqa: E731
+            self.top_send, self.bot_send, self.top_recv, self.bot_recv = mk(), mk(), mk(), mk()
 
     @property
     def halo_valid(self) -> int:
         return self.engine.halo_valid
 
     def step(self, n: int):
+        self._views = None                     # board pointers move with every step
         self.engine.step(n)
 
     def stream_context(self):
         return torch.cuda.stream(self.stream)
 
+    def _board_views(self):
+        if self._views is None:
+            ptrs, self.layout = self.engine.halo_buffers()
+            self._views = tuple(torch.as_tensor(_DeviceRows(p, self._shape), device=self.device)
+                                for p in ptrs)
+        return self._views
+
     def export_rows(self):
+        if self.zero_copy:
+            st, sb, _, _ = self._board_views()
+            return st, sb
         s = self.stream.cuda_stream
         self.engine.export_halo(self.top_send.data_ptr(), self.bot_send.data_ptr(), s)
         return self.top_send, self.bot_send
 
     def recv_buffers(self):
+        if self.zero_copy:
+            _, _, rt, rb = self._board_views()
+            return rt, rb
         return self.top_recv, self.bot_recv
 
     def import_rows(self, top, bottom):
+        if self.zero_copy:
+            _, _, rt, rb = self._board_views()
+            if top.data_ptr() != rt.data_ptr():
+                rt.copy_(top, non_blocking=True)
+            if bottom.data_ptr() != rb.data_ptr():
+                rb.copy_(bottom, non_blocking=True)
+            self.engine.halo_done()
+            return
         s = self.stream.cuda_stream
         if top.device != self.device:
             self.top_recv.copy_(top, non_blocking=True)
@@ -81,6 +125,7 @@ class DistStrip:
         # gloo cannot move device tensors: stage the K-row messages through host memory
         self.stage_on_host = stage_on_host
         self.exchanges = 0
+        self._layout_checked = False
 
     def exchange(self):
         ctx = getattr(self.strip, "stream_context", None)
@@ -89,9 +134,26 @@ class DistStrip:
         with ctx():
             return self._exchange()
 
+    def _check_layout(self, like):
+        """Zero-copy messages carry the engines' stepping layout: every rank must agree
+        (equal width, halo and flags guarantee it; checked once, before the first
+        exchange, with one tiny all-reduce)."""
+        self._layout_checked = True
+        lay = getattr(self.strip, "layout", None)
+        if lay is None:
+            return
+        dev = like.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([lay], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, group=self.group)
+        if int(t.item()) not in (0, self.world):
+            raise RuntimeError(f"rank {self.rank}: halo layouts differ across ranks "
+                               f"(sum {int(t.item())} of {self.world})")
+
     def _exchange(self):
         top, bot = self.strip.export_rows()
         top_recv, bot_recv = self.strip.recv_buffers()
+        if not self._layout_checked:
+            self._check_layout(top)
         if self.stage_on_host:
             top, bot = top.cpu(), bot.cpu()
             top_recv, bot_recv = torch.empty_like(top), torch.empty_like(bot)

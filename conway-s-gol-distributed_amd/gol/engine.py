@@ -163,6 +163,16 @@ class Engine:
     def halo_done(self):
         self._c(self._L.gol_halo_done(self._h))
 
+    def halo_buffers(self):
+        """Zero-copy exchange: device pointers (send_top, send_bottom, recv_top,
+        recv_bottom) into the current board, each halo x words_per_row uint64, and the
+        rows' layout (0 standard, 1 interleaved).  Valid until the next step."""
+        p = [ctypes.c_void_p() for _ in range(4)]
+        lay = ctypes.c_int32()
+        self._c(self._L.gol_halo_buffers(self._h, *(ctypes.byref(x) for x in p),
+                                         ctypes.byref(lay)))
+        return tuple(int(x.value or 0) for x in p), int(lay.value)
+
 
 def strip_split(height: int, n: int):
     """The reference Server's row split (Server/gol/distributor.go:106-116):

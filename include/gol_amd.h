@@ -156,6 +156,19 @@ int gol_copy_halo_from_upper(gol_ctx *dst, gol_ctx *src);
 int gol_copy_halo_from_lower(gol_ctx *dst, gol_ctx *src);
 /* Mark the halos fresh after all copies into this engine are enqueued. */
 int gol_halo_done(gol_ctx *ctx);
+/* Zero-copy exchange (the RCCL path: the transport reads and writes the board
+ * itself).  Device pointers into the current board buffer: send_top / send_bottom =
+ * the first / last `halo` owned rows, recv_top / recv_bottom = the top / bottom halo
+ * rows, each halo x words_per_row uint64 with row stride words_per_row.  The rows
+ * are in the engine's stepping layout (converted to it here if needed), returned in
+ * *layout (0 standard, 1 interleaved): both ends of an exchange must report the
+ * same layout -- engines created with the same width, halo and flags do.  The
+ * pointers are valid until the next gol_step / gol_load*.  Order the transport after
+ * the engine's stream, and the next gol_step after the receives, then call
+ * gol_halo_done.  Replaces the per-turn strip+halo RPC copy
+ * (reference Server/gol/distributor.go:185-224). */
+int gol_halo_buffers(gol_ctx *ctx, void **send_top, void **send_bottom, void **recv_top,
+                     void **recv_bottom, int32_t *layout);
 
 /* -------------------------------------------------------------- run driver */
 typedef struct gol_params {          /* Local/gol/gol.go:4-9 */

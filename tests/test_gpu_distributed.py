@@ -11,16 +11,74 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("world,halo,tpl", [(2, 6, 4), (2, 5, 1), (3, 5, 1), (3, 7, 6), (4, 8, 8)])
-def test_torchrun_strips_one_gpu(world, halo, tpl):
+def _dist_check(world, args, port):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={world}", "--master-addr=127.0.0.1", f"--master-port={29500 + world}",
-           os.path.join(ROOT, "tools", "dist_check.py"), "--halo", str(halo), "--tpl", str(tpl)]
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.join(ROOT, "tools", "dist_check.py")] + [str(x) for x in args]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0, p.stdout[-6000:] + "\n----- stderr -----\n" + "\n".join(
         ln for ln in p.stderr.splitlines() if "amdgpu.ids" not in ln and "socket.cpp" not in ln)[:6000]
     assert "equal=True" in p.stdout
+    return p.stdout
+
+
+@pytest.mark.parametrize("world,halo,tpl,copy", [(2, 6, 4, False), (2, 5, 1, False),
+                                                 (3, 5, 1, True), (3, 7, 6, False),
+                                                 (4, 8, 8, False), (2, 8, 8, True)])
+def test_torchrun_strips_one_gpu(world, halo, tpl, copy):
+    """gloo, host-staged; zero-copy board views (default) and the export/import copies."""
+    _dist_check(world, ["--halo", halo, "--tpl", tpl] + (["--copy"] if copy else []),
+                29500 + world + (10 if copy else 0))
+
+
+@pytest.mark.parametrize("halo,tpl,copy", [(8, 8, False), (16, 8, False), (5, 1, False),
+                                           (6, 6, False), (8, 8, True)])
+def test_rccl_self_exchange(halo, tpl, copy):
+    """The RCCL exchange proper (backend nccl, batch_isend_irecv on device tensors, the
+    engine's own stream) at world size 1: rank 0 is its own up and down neighbour, so
+    its halos come back over RCCL from its own boundary rows -- the N = 1 torus.  Zero-copy
+    (RCCL reads/writes the board rows in place, interleaved layout at tpl > 1) and the
+    copy path.  Bit-exact against the oracle after 53 turns (several exchanges)."""
+    out = _dist_check(1, ["--backend", "nccl", "--halo", halo, "--tpl", tpl, "--height", 640]
+                      + (["--copy"] if copy else []), 29530 + halo + (50 if copy else 0))
+    assert "backend=nccl" in out
+    if not copy:
+        assert f"layout={1 if tpl > 1 else 0}" in out
+
+
+def test_halo_buffers_zero_copy_torus():
+    """gol_halo_buffers: the four views are the strip's boundary and halo rows in the
+    current board; copying send_bottom -> recv_top and send_top -> recv_bottom on the
+    engine's stream (a strip that is its own neighbour) and stepping reproduces the
+    torus exactly, across layouts (tpl 8 = interleaved, 1 = standard)."""
+    import numpy as np
+    import torch
+    for p in (os.path.join(ROOT, "conway-s-gol-distributed_amd"), ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from gol.distributed import EngineStrip, make_engine_strip
+    from oracle import oracle as O
+    dev = torch.device("cuda", 0)
+    for tpl, halo in ((8, 16), (1, 3), (6, 12)):
+        W, H, turns = 1536, 300, 41
+        eng = make_engine_strip(W, H, 0, 1, halo, 0, turns_per_launch=tpl)
+        es = EngineStrip(eng, dev)
+        eng.fill_random(11)
+        with es.stream_context():
+            left = turns
+            while left:
+                if es.halo_valid == 0:
+                    st, sb = es.export_rows()
+                    es.import_rows(sb, st)
+                n = min(left, es.halo_valid)
+                es.step(n)
+                left -= n
+        got = eng.read_packed()
+        eng.close()
+        want = O.bit_run(O.gen_random(11, W, H), W, turns)
+        assert np.array_equal(got, want), (tpl, halo)
+        assert es.layout == (1 if tpl > 1 else 0)
 
 
 REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",

@@ -2,7 +2,9 @@
 """Multi-rank strip rehearsal on ONE GPU: torchrun N ranks, every rank's engine on
 cuda:0, halos exchanged through gol.distributed.DistStrip over gloo (staged via host
 memory), final board gathered to rank 0 and compared with the CPU oracle.
-Used by tests/test_gpu_distributed.py; the RCCL path differs only in the backend."""
+`--backend nccl` runs the RCCL path proper (zero-copy board views, batch_isend_irecv);
+on a one-GPU box that is world size 1, where rank 0 exchanges with itself.
+Used by tests/test_gpu_distributed.py."""
 import argparse
 import os
 import sys
@@ -23,30 +25,41 @@ def main():
     ap.add_argument("--halo", type=int, default=6)
     ap.add_argument("--tpl", type=int, default=4)
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--backend", choices=("gloo", "nccl"), default="gloo")
+    ap.add_argument("--copy", action="store_true", help="export/import copies, not zero-copy")
     a = ap.parse_args()
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
+    if a.backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    gdev = dev if a.backend == "nccl" else "cpu"
     import gol
     from gol.distributed import DistStrip, EngineStrip, make_engine_strip
     eng = make_engine_strip(a.size, a.height, rank, world, a.halo, 0, turns_per_launch=a.tpl)
     eng.fill_random(a.seed)
-    ds = DistStrip(EngineStrip(eng, dev), rank, world, stage_on_host=True)
+    ds = DistStrip(EngineStrip(eng, dev, zero_copy=not a.copy), rank, world,
+                   stage_on_host=a.backend == "gloo")
     ds.step(a.turns)
     split = gol.strip_split(a.height, world)
     maxr = max(r for _, r in split)
-    mine = torch.zeros((maxr, eng.words_per_row), dtype=torch.int64)   # gloo gather: equal sizes
+    mine = torch.zeros((maxr, eng.words_per_row), dtype=torch.int64)   # gather: equal sizes
     mine[: eng.rows] = torch.from_numpy(eng.read_packed().view(np.int64))
-    parts = [torch.zeros((maxr, eng.words_per_row), dtype=torch.int64) for _ in split]
+    mine = mine.to(gdev)
+    parts = [torch.zeros((maxr, eng.words_per_row), dtype=torch.int64, device=gdev)
+             for _ in split]
     if rank == 0:
         dist.gather(mine, parts, dst=0)
-        got = np.concatenate([p.numpy()[:r] for p, (_, r) in zip(parts, split)]).view(np.uint64)
+        got = np.concatenate([p.cpu().numpy()[:r]
+                              for p, (_, r) in zip(parts, split)]).view(np.uint64)
         from oracle import oracle as O
         want = O.bit_run(O.gen_random(a.seed, a.size, a.height), a.size, a.turns)
         ok = np.array_equal(got, want)
-        print(f"dist_check world={world} halo={eng.halo} exchanges={ds.exchanges} "
-              f"tpl={a.tpl} equal={ok}", flush=True)
+        print(f"dist_check backend={a.backend} world={world} halo={eng.halo} "
+              f"exchanges={ds.exchanges} tpl={a.tpl} layout={ds.strip.layout} equal={ok}",
+              flush=True)
         if not ok:
             sys.exit(1)
     else:
