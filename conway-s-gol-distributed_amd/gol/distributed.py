@@ -7,8 +7,11 @@ halo row above and below through the Server (``:185-224``).  Here every rank
 keeps its strip resident on its own MI355X with ``halo`` = K extra rows above and
 below, runs K turns locally (the valid region shrinks by one row per turn), and
 then exchanges only the K boundary rows with its ring neighbours
-(r-1) mod N and (r+1) mod N — RCCL send/recv over xGMI on GPUs (backend "nccl"),
-gloo on CPU for tests.  Results are identical to the single-GPU torus for any N
+(r-1) mod N and (r+1) mod N — RCCL send/recv over xGMI on GPUs, gloo on CPU for
+tests.  On GPUs the messages are the board rows themselves (zero-copy views,
+``gol_halo_buffers``) and the sends/receives are enqueued by direct RCCL calls on
+the engine's stream (``gol.rccl``); torch's ``batch_isend_irecv`` remains as the
+alternative transport.  Results are identical to the single-GPU torus for any N
 because the rows owned after every K-turn block are exactly the torus rows.
 
 Message order is the same on every rank — send-up, recv-from-down, send-down,
@@ -116,8 +119,13 @@ class EngineStrip:
 class DistStrip:
     """One rank's strip; ``step(turns)`` interleaves local turns and halo exchanges."""
 
-    def __init__(self, strip, rank: int, world: int, group=None, stage_on_host: bool = False):
+    def __init__(self, strip, rank: int, world: int, group=None, stage_on_host: bool = False,
+                 rccl=None):
+        """``rccl``: a gol.rccl.RcclComm -- the exchange is enqueued by direct RCCL calls on
+        the strip's own stream (no cross-stream waits); None = torch.distributed
+        point-to-point (batch_isend_irecv on the nccl backend, isend/irecv on gloo)."""
         self.strip = strip
+        self.rccl = rccl
         self.rank, self.world = int(rank), int(world)
         self.up = (self.rank - 1) % self.world
         self.down = (self.rank + 1) % self.world
@@ -154,6 +162,14 @@ class DistStrip:
         top_recv, bot_recv = self.strip.recv_buffers()
         if not self._layout_checked:
             self._check_layout(top)
+        if self.rccl is not None:
+            nbytes = top.numel() * top.element_size()
+            self.rccl.exchange([(top.data_ptr(), self.up), (bot.data_ptr(), self.down)],
+                               [(bot_recv.data_ptr(), self.down), (top_recv.data_ptr(), self.up)],
+                               nbytes, self.strip.stream.cuda_stream)
+            self.strip.import_rows(top_recv, bot_recv)
+            self.exchanges += 1
+            return
         if self.stage_on_host:
             top, bot = top.cpu(), bot.cpu()
             top_recv, bot_recv = torch.empty_like(top), torch.empty_like(bot)

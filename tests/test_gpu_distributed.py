@@ -32,17 +32,20 @@ def test_torchrun_strips_one_gpu(world, halo, tpl, copy):
                 29500 + world + (10 if copy else 0))
 
 
-@pytest.mark.parametrize("halo,tpl,copy", [(8, 8, False), (16, 8, False), (5, 1, False),
-                                           (6, 6, False), (8, 8, True)])
-def test_rccl_self_exchange(halo, tpl, copy):
-    """The RCCL exchange proper (backend nccl, batch_isend_irecv on device tensors, the
-    engine's own stream) at world size 1: rank 0 is its own up and down neighbour, so
-    its halos come back over RCCL from its own boundary rows -- the N = 1 torus.  Zero-copy
-    (RCCL reads/writes the board rows in place, interleaved layout at tpl > 1) and the
-    copy path.  Bit-exact against the oracle after 53 turns (several exchanges)."""
-    out = _dist_check(1, ["--backend", "nccl", "--halo", halo, "--tpl", tpl, "--height", 640]
-                      + (["--copy"] if copy else []), 29530 + halo + (50 if copy else 0))
-    assert "backend=nccl" in out
+@pytest.mark.parametrize("halo,tpl,copy,transport", [
+    (8, 8, False, "rccl"), (16, 8, False, "rccl"), (5, 1, False, "rccl"), (6, 6, False, "rccl"),
+    (8, 8, True, "rccl"), (8, 8, False, "torch"), (5, 1, True, "torch")])
+def test_rccl_self_exchange(halo, tpl, copy, transport):
+    """The RCCL exchange proper (backend nccl, device buffers) at world size 1: rank 0 is
+    its own up and down neighbour, so its halos come back over RCCL from its own boundary
+    rows -- the N = 1 torus.  Transports: direct RCCL send/recv on the engine's stream
+    (gol.rccl, the bench default) and torch batch_isend_irecv; zero-copy board views
+    (interleaved layout at tpl > 1) and the copy path.  Bit-exact against the oracle
+    after 53 turns (several exchanges)."""
+    port = 29530 + halo + (50 if copy else 0) + (100 if transport == "torch" else 0)
+    out = _dist_check(1, ["--backend", "nccl", "--halo", halo, "--tpl", tpl, "--height", 640,
+                          "--transport", transport] + (["--copy"] if copy else []), port)
+    assert "backend=nccl" in out and f"transport={transport}" in out
     if not copy:
         assert f"layout={1 if tpl > 1 else 0}" in out
 

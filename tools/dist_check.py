@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--backend", choices=("gloo", "nccl"), default="gloo")
     ap.add_argument("--copy", action="store_true", help="export/import copies, not zero-copy")
+    ap.add_argument("--transport", choices=("rccl", "torch"), default="rccl",
+                    help="nccl backend: direct RCCL on the engine stream, or batch_isend_irecv")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -40,8 +42,12 @@ def main():
     from gol.distributed import DistStrip, EngineStrip, make_engine_strip
     eng = make_engine_strip(a.size, a.height, rank, world, a.halo, 0, turns_per_launch=a.tpl)
     eng.fill_random(a.seed)
+    comm = None
+    if a.backend == "nccl" and a.transport == "rccl":
+        from gol.rccl import RcclComm
+        comm = RcclComm(rank, world, dev)
     ds = DistStrip(EngineStrip(eng, dev, zero_copy=not a.copy), rank, world,
-                   stage_on_host=a.backend == "gloo")
+                   stage_on_host=a.backend == "gloo", rccl=comm)
     ds.step(a.turns)
     split = gol.strip_split(a.height, world)
     maxr = max(r for _, r in split)
@@ -57,13 +63,15 @@ def main():
         from oracle import oracle as O
         want = O.bit_run(O.gen_random(a.seed, a.size, a.height), a.size, a.turns)
         ok = np.array_equal(got, want)
-        print(f"dist_check backend={a.backend} world={world} halo={eng.halo} "
+        print(f"dist_check backend={a.backend} transport={a.transport if comm else 'torch'} world={world} halo={eng.halo} "
               f"exchanges={ds.exchanges} tpl={a.tpl} layout={ds.strip.layout} equal={ok}",
               flush=True)
         if not ok:
             sys.exit(1)
     else:
         dist.gather(mine, dst=0)
+    if comm is not None:
+        comm.close()
     eng.close()
     dist.destroy_process_group()
 

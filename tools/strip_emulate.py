@@ -27,8 +27,24 @@ def main():
     ap.add_argument("--turns", type=int, default=768)
     ap.add_argument("--tpl", default="0")
     ap.add_argument("--band", default="0")
+    ap.add_argument("--rccl", choices=("", "direct", "torch"), default="",
+                    help="exchange through RCCL at world size 1 (rank 0 is its own neighbour, "
+                         "zero-copy board views): direct RCCL calls on the engine stream, or "
+                         "torch batch_isend_irecv; default: local copies")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    ds_for = None
+    if a.rccl:
+        import torch.distributed as dist
+        from gol.distributed import DistStrip
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29641")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        comm = None
+        if a.rccl == "direct":
+            from gol.rccl import RcclComm
+            comm = RcclComm(0, 1, dev)
+        ds_for = lambda es: DistStrip(es, 0, 1, rccl=comm)  # noqa: E731
     if a.full:
         e = gol.Engine(a.size, a.size, device=0)
         e.fill_random(3)
@@ -53,8 +69,11 @@ def main():
                                     band_rows=band)
             es = EngineStrip(eng, dev)
             eng.fill_random(3)
+            ds = ds_for(es) if ds_for else None
             with torch.cuda.stream(es.stream):
                 def run(turns):
+                    if ds is not None:
+                        return ds.step(turns)
                     left = turns
                     while left:
                         if es.halo_valid == 0:
@@ -73,7 +92,8 @@ def main():
             info = eng.info()
             print(json.dumps({"n": n, "halo": info.halo, "rows": info.rows, "band": info.band_rows,
                               "tpl": info.turns_per_launch, "us_per_turn": round(us, 2),
-                              "aggregate_GCUPS_upper": round(a.size * a.size / us / 1e3, 1)}),
+                              "aggregate_GCUPS_upper": round(a.size * a.size / us / 1e3, 1),
+                              "exchange": f"rccl-self-{a.rccl}" if ds else "local-copy"}),
                   flush=True)
             eng.close()
 
