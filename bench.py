@@ -137,7 +137,21 @@ def main():
         comm = None
         if a.backend == "nccl" and a.transport == "rccl":
             from gol.rccl import RcclComm
-            comm = RcclComm(rank, world, dev)
+            ok = 1
+            try:
+                comm = RcclComm(rank, world, dev)
+            except (OSError, RuntimeError) as e:     # no usable librccl symbols / init error
+                print(f"[rank {rank}] direct RCCL unavailable ({e}); using torch "
+                      "batch_isend_irecv", file=sys.stderr)
+                ok = 0
+            # every rank must pick the same transport
+            flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                if comm is not None:
+                    comm.close()
+                comm = None
+                a.transport = "torch"
         runner = DistStrip(EngineStrip(eng, dev, stream), rank, world,
                            stage_on_host=a.backend == "gloo", rccl=comm)
         rows_local = eng.rows
