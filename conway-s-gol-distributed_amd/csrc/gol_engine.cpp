@@ -172,7 +172,7 @@ void autotune_multi(gol_ctx *c, bool tune_k)
 {
     const long long words = (long long)c->buf_rows * c->pitch;
     if (words < (1ll << 20)) return;                 // < 64 Mi cells: keep the defaults
-    static const int kKs[] = {6, 8};
+    static const int kKs[] = {6, 8};   // K = 7 measured no faster (DESIGN)
     static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
     // plus the bands whose grid just fits 1..4 rounds of resident wavefronts (65536^2 at 4
     // waves/SIMD: 274 -> 4080 of 4096 waves, 137 -> 8160 of 8192)
@@ -182,7 +182,7 @@ void autotune_multi(gol_ctx *c, bool tune_k)
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
         const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
         const long long ntx = golk::multi_tiles(c->cfg.width, lane_dw);
-        for (int K : {6, 8}) {
+        for (int K : kKs) {
             const long long cap =
                 (long long)ncu * 4 * golk::multi_blocks_per_cu(K, c->multi_words, c->multi_variant);
             for (int r = 1; r <= 4 && cap > 0; ++r) {
@@ -576,7 +576,6 @@ int gol_step(gol_ctx *c, int64_t turns)
             // tpl 6 run as 18 x 6 + 4 x 5, not 21 x 6 + 2
             const int64_t nl = (room + c->tpl - 1) / c->tpl;
             k = (int)((room + nl - 1) / nl);
-            if (k == 7) k = 6;                     // supported depths: 2..6, 8
             if (!golk::multi_ok(c->cfg.width, k)) k = 1;
         }
         // rows computed: torus -> all; strip -> [s, buf_rows - s) after turn s since exchange

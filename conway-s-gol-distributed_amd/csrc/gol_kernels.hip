@@ -1325,6 +1325,7 @@ static void *multi_fn(int turns, int variant)
         case 4: return reinterpret_cast<void *>(&k_step_multi<4, V>);
         case 5: return reinterpret_cast<void *>(&k_step_multi<5, V>);
         case 6: return reinterpret_cast<void *>(&k_step_multi<6, V>);
+        case 7: return reinterpret_cast<void *>(&k_step_multi<7, V>);
         case 8: return reinterpret_cast<void *>(&k_step_multi<8, V>);
         default: return nullptr;
         }
@@ -1346,6 +1347,7 @@ static void *multi_fn(int turns, int variant)
         case 4: return skew_fn<4, 2, kMultiSkewILW16>();
         case 5: return skew_fn<5, 2, kMultiSkewILW16>();
         case 6: return skew_fn<6, 2, kMultiSkewILW16>();
+        case 7: return skew_fn<7, 2, kMultiSkewILW16>();
         case 8: return skew_fn<8, 2, kMultiSkewILW16>();
         default: return nullptr;
         }
@@ -1357,6 +1359,7 @@ static void *multi_fn(int turns, int variant)
         case 4: return skew_fn<4, 2, kMultiSkewIL>();
         case 5: return skew_fn<5, 2, kMultiSkewIL>();
         case 6: return skew_fn<6, 2, kMultiSkewIL>();
+        case 7: return skew_fn<7, 2, kMultiSkewIL>();
         case 8: return skew_fn<8, 2, kMultiSkewIL>();
         default: return nullptr;
         }
@@ -1386,6 +1389,7 @@ static void *multi_fn(int turns, int variant)
     case 4: return skew_fn<4, 2 * V, kMultiSkew>();
     case 5: return skew_fn<5, 2 * V, kMultiSkew>();
     case 6: return skew_fn<6, 2 * V, kMultiSkew>();
+    case 7: return skew_fn<7, 2 * V, kMultiSkew>();
     case 8: return skew_fn<8, 2 * V, kMultiSkew>();
     default: return nullptr;
     }

@@ -133,7 +133,7 @@ def test_stencil_variants(gol, oracle, monkeypatch, variant, w, h, band):
 
 
 @pytest.mark.parametrize("mw", [1, 2])
-@pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 8])
+@pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 17), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (1024, 1, 5, 8), (512, 130, 1000, 24)])
 def test_temporal_blocking(gol, oracle, monkeypatch, mw, tpl, w, h, band, turns):
@@ -190,7 +190,7 @@ def test_il_layout_roundtrip():
 
 
 @pytest.mark.parametrize("mv", [6, 7])
-@pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 8])
+@pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 19), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (2048, 300, 137, 17),
                                             (8064, 33, 16, 8), (7936, 20, 9, 16)])

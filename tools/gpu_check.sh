@@ -35,6 +35,9 @@ for step in "$@"; do
     tbq16k) run tbq16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 0,16,20,24,32,48 --tpl 4,6,8 --mw 1 --turns 960 ;;
     skew)   run skew 500 python -u tools/sweep.py --variants 2 --bands 96,137,192 --tpl 6,8 --mw 1 --mv 0,1,2,3,4 --turns 240 ;;
     skew16k) run skew16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 16,20,24,32 --tpl 6,8 --mw 1 --mv 0,1,2,3,4 --turns 960 ;;
+    tb7)    run tb7 400 python -u -m pytest tests/test_gpu_engine.py -v -k temporal_blocking --timeout 150 --timeout-method thread ;;
+    bench78) run bench_k7 300 python -u bench.py --tpl 7 --no-cpu-baseline && run bench_k8 300 python -u bench.py --tpl 8 --no-cpu-baseline && run bench_auto 300 python -u bench.py --no-cpu-baseline ;;
+    strips78) run strips78 400 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --tpl 0,7,8 --rccl direct ;;
     calib)  run calib 300 bash tools/calib/run.sh ;;
     sweep)  run sweep 400 python -u tools/sweep.py --variants 2,4,5,6 --bands 16,32,64,128,256 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
