@@ -194,10 +194,11 @@ def main():
     # section 8(d): the judged figure uses the k = 1 definition, 0.25 B per cell-update (1 bit
     # read + 1 bit written), times the cell-updates one launch performs (turns / launches
     # x cells: K when every launch runs K turns; the engine spreads turns evenly, so a
-    # remainder makes a few launches shallower), divided by the average launch duration (HIP events of the timed region on the engine's stream
-    # / launches).  With temporal blocking the kernel itself moves only one read + one
-    # write of the packed board per launch (0.25 B x cells): reported as `board_*`, with
-    # the PMC-measured bytes in `traffic`.
+    # remainder makes a few launches shallower), divided by the average launch duration
+    # (HIP events of the timed region on the engine's stream / launches).  With temporal
+    # blocking the kernel itself moves only one read + one write of the packed board per
+    # launch (0.25 B x cells): reported as `board_*`, with the PMC-measured bytes in
+    # `traffic`.
     cells_local = rows_local * W
     launch_us = gpu_ms * 1e3 / max(launches, 1)
     traffic, traffic_src = pmc_traffic(W, K)
