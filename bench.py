@@ -14,10 +14,14 @@ and each rank exchanges `--halo` boundary rows with its ring neighbours over
 RCCL every `--halo` turns ("strong" scaling: the total board is fixed).
 
 Printed (rank 0): one JSON line with the driver's contract fields plus
-`roofline` (algorithmic 0.25 B per cell-update, the k = 1 definition, vs 8 TB/s HBM;
-the blocked kernel's own board traffic as `board_*`), `valu_roofline` and
-`cpu_baseline` (oracle/refcpu.c, the C restatement of the reference's CPU path,
-timed on a bounded sample on this host).
+`roofline` (the dominant kernel's algorithmic HBM bytes per launch -- one read + one
+write of the packed board, 0.25/k B per cell-update for k fused turns -- per average
+launch time, vs 8 TB/s; PMC-measured bytes in `traffic`), `k1_equivalent` (the k = 1
+bytes of SURVEY 8(d), which exceed any HBM roof once k > 1), `valu_roofline` (the
+binding roof of the blocked kernel), `configs_measured` (BASELINE configs[2]: the
+16384^2 board, 10000 turns, same N) and `cpu_baseline` (oracle/refcpu.c, the C
+restatement of the reference's CPU path, timed on a bounded sample on this host's CPU
+share).
 """
 import argparse
 import json
@@ -61,7 +65,17 @@ def parse():
                     help="turns per stencil launch (temporal blocking; 0 = engine default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-turns", type=int, default=2)
-    ap.add_argument("--cpu-cores", type=int, default=16)
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="threads for the CPU baseline (0 = this host's CPU share: the "
+                         "affinity mask, capped by OMP_NUM_THREADS when that is set)")
+    ap.add_argument("--c3-size", type=int, default=16384,
+                    help="board side of the second measured config (BASELINE configs[2]; "
+                         "0 = skip)")
+    ap.add_argument("--c3-turns", type=int, default=10000,
+                    help="turns of the second config (configs[2]: 10000)")
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="N > 1, direct RCCL: overlap the halo exchange with the first "
+                         "launch's interior rows (gol_step_overlap); 0 = serialised")
     ap.add_argument("--transport", choices=("rccl", "torch"), default="rccl",
                     help="N > 1 halo transport on the nccl backend: direct RCCL send/recv on "
                          "the engine's stream (default) or torch batch_isend_irecv")
@@ -84,11 +98,24 @@ def pmc_traffic(size, k):
     return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def cpu_share():
+    """(threads to use, affinity-mask CPUs, OMP_NUM_THREADS or None): the GPU box's CPU
+    share for one GPU is OMP_NUM_THREADS (16) while its affinity mask lists every CPU of
+    the host, so the share caps the mask."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return share, aff, (int(omp) if omp and omp.isdigit() else None)
+
+
 def cpu_baseline(size, seed, turns, cores):
     """oracle/refcpu.c (literal restatement of the reference's Server/SubServer CPU path,
-    4 sub-servers as in the reference's default SUB list, Threads = cores) on the same
-    board for a bounded number of turns."""
+    4 sub-servers as in the reference's default SUB list, Threads = the core count) on the
+    same board for a bounded number of turns."""
     from oracle import oracle as O
+    share, aff, omp = cpu_share()
+    if cores <= 0:
+        cores = share
     board = O.unpack(O.gen_random(seed, size, size), size)
     t0 = time.perf_counter()
     O.ref_run(board, turns, nsub=4, threads=cores, ncores=cores)
@@ -97,7 +124,92 @@ def cpu_baseline(size, seed, turns, cores):
     return {"value": round(size * size * turns / dt / 1e9, 4), "unit": "GCUPS",
             "cores": cores, "kind": "port",
             "sample": f"{size}x{size} random board seed {seed}, {turns} turns, oracle/refcpu.c "
-                      f"(4 sub-servers x {cores} threads, no gob/HTTP: optimistic), {dt:.1f} s"}
+                      f"(4 sub-servers x Threads={cores} goroutine-equivalents on {cores} "
+                      f"OpenMP threads; host affinity mask {aff} CPUs, OMP_NUM_THREADS "
+                      f"{omp}; no gob/HTTP: optimistic), {dt:.1f} s"}
+
+
+def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
+    """Time `steps` turns of one size x size torus board (whole board at N = 1, this rank's
+    row strip at N > 1) after `warmup` turns.  Returns the timing and roofline inputs."""
+    import gol
+    from gol.distributed import DistStrip, EngineStrip, make_engine_strip
+
+    W = H = size
+    comm = None
+    if world == 1:
+        eng = gol.Engine(W, H, device=gpu, band_rows=a.band, turns_per_launch=a.tpl)
+        eng.set_stream(stream.cuda_stream)
+        eng.fill_random(a.seed)
+        runner = eng
+        rows_local = H
+        transport = ""
+    else:
+        eng = make_engine_strip(W, H, rank, world, a.halo, gpu, band_rows=a.band,
+                                turns_per_launch=a.tpl)
+        eng.fill_random(a.seed)
+        transport = a.transport
+        if a.backend == "nccl" and transport == "rccl":
+            from gol.rccl import RcclComm
+            try:
+                comm = RcclComm(rank, world, dev)   # raises on every rank together
+            except (OSError, RuntimeError) as e:
+                if rank == 0:
+                    print(f"direct RCCL unavailable ({e}); using torch batch_isend_irecv",
+                          file=sys.stderr)
+                comm, transport = None, "torch"
+        runner = DistStrip(EngineStrip(eng, dev, stream), rank, world,
+                           stage_on_host=a.backend == "gloo", rccl=comm,
+                           overlap=bool(a.overlap))
+        rows_local = eng.rows
+        # set up the RCCL p2p connections outside the timed region: one halo exchange now
+        # (all strips hold their true halo rows after fill_random, so it changes nothing)
+        runner.exchange()
+    runner.step(warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier(device_ids=dev_ids)
+    torch.cuda.synchronize(dev)
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    launches0 = eng.info().launches
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    runner.step(steps)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier(device_ids=dev_ids)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    info = eng.info()
+    launches = info.launches - launches0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64,
+                         device=dev if a.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    overlap = bool(getattr(runner, "overlap", False))
+    if comm is not None:
+        comm.close()
+    out = {"W": W, "H": H, "steps": steps, "wall": wall, "gpu_ms": gpu_ms,
+           "launches": launches, "K": info.turns_per_launch, "rows_local": rows_local,
+           "band": info.band_rows, "fast": bool(info.fast_path), "halo": info.halo,
+           "transport": transport, "overlap": overlap}
+    eng.close()
+    return out
+
+
+def parallelism(a, world, m):
+    if world == 1:
+        return "row-strips x1"
+    how = ({"rccl": "RCCL send/recv on the engine stream" + (
+                ", overlapped with the interior rows" if m["overlap"] else ""),
+            "torch": "RCCL via torch batch_isend_irecv"}[m["transport"]]
+           if a.backend == "nccl" else "gloo host-staged")
+    return f"row-strips x{world}, halo {m['halo']}, {how}"
 
 
 def main():
@@ -116,100 +228,34 @@ def main():
         else:
             dist.init_process_group("gloo")
     dev_ids = [gpu] if a.backend == "nccl" else None
-
-    import gol
-    from gol.distributed import DistStrip, EngineStrip, make_engine_strip
-
-    W = H = a.size
     # a dedicated (non-default) stream shared by the engine, the events and RCCL
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    if world == 1:
-        eng = gol.Engine(W, H, device=gpu, band_rows=a.band, turns_per_launch=a.tpl)
-        eng.set_stream(stream.cuda_stream)
-        eng.fill_random(a.seed)
-        runner = eng
-        rows_local = H
-    else:
-        eng = make_engine_strip(W, H, rank, world, a.halo, gpu, band_rows=a.band,
-                                turns_per_launch=a.tpl)
-        eng.fill_random(a.seed)
-        comm = None
-        if a.backend == "nccl" and a.transport == "rccl":
-            from gol.rccl import RcclComm
-            ok = 1
-            try:
-                comm = RcclComm(rank, world, dev)
-            except (OSError, RuntimeError) as e:     # no usable librccl symbols / init error
-                print(f"[rank {rank}] direct RCCL unavailable ({e}); using torch "
-                      "batch_isend_irecv", file=sys.stderr)
-                ok = 0
-            # every rank must pick the same transport
-            flag = torch.tensor([ok], dtype=torch.int32, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if int(flag.item()) == 0:
-                if comm is not None:
-                    comm.close()
-                comm = None
-                a.transport = "torch"
-        runner = DistStrip(EngineStrip(eng, dev, stream), rank, world,
-                           stage_on_host=a.backend == "gloo", rccl=comm)
-        rows_local = eng.rows
-    info = eng.info()
 
-    if world > 1:
-        # set up the RCCL p2p connections outside the timed region: one halo exchange now
-        # (all strips hold their true halo rows after fill_random, so it changes nothing)
-        runner.exchange()
-    runner.step(a.warmup)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier(device_ids=dev_ids)
-    torch.cuda.synchronize(dev)
-
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    launches0 = eng.info().launches
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    runner.step(a.steps)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier(device_ids=dev_ids)
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    gpu_ms = ev0.elapsed_time(ev1)
-    info = eng.info()
-    launches = info.launches - launches0
-    K = info.turns_per_launch
-
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64,
-                         device=dev if a.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-
-    # Dominant kernel: one launch = K turns over this rank's rows.  Roofline per SURVEY.md
-    # section 8(d): the judged figure uses the k = 1 definition, 0.25 B per cell-update (1 bit
-    # read + 1 bit written), times the cell-updates one launch performs (turns / launches
-    # x cells: K when every launch runs K turns; the engine spreads turns evenly, so a
-    # remainder makes a few launches shallower), divided by the average launch duration
-    # (HIP events of the timed region on the engine's stream / launches).  With temporal
-    # blocking the kernel itself moves only one read + one write of the packed board per
-    # launch (0.25 B x cells): reported as `board_*`, with the PMC-measured bytes in
-    # `traffic`.
-    cells_local = rows_local * W
-    launch_us = gpu_ms * 1e3 / max(launches, 1)
-    traffic, traffic_src = pmc_traffic(W, K)
-    turns_per_launch = a.steps / max(launches, 1)
-    bytes_k1 = BYTES_PER_CELL_UPDATE * turns_per_launch * cells_local
-    bytes_board = BYTES_PER_CELL_UPDATE * cells_local
-    achieved = bytes_k1 / (launch_us * 1e-6) / 1e9
-    board_achieved = bytes_board / (launch_us * 1e-6) / 1e9
-    gcups = W * H * a.steps / wall / 1e9
+    m = measure(a, a.size, a.steps, a.warmup, world, rank, gpu, dev, dev_ids, stream)
+    c3 = None
+    if a.c3_size > 0 and a.c3_size != a.size:
+        c3 = measure(a, a.c3_size, a.c3_turns, max(a.warmup, 60), world, rank, gpu, dev,
+                     dev_ids, stream)
 
     if rank == 0:
+        W, H, K = m["W"], m["H"], m["K"]
+        gcups = W * H * a.steps / m["wall"] / 1e9
+        # Dominant kernel: one launch = turns/launches turns over this rank's rows.
+        # Roofline (HBM): the bytes the blocked kernel must move per launch are one read and
+        # one write of the packed board -- 0.25/k B per cell-update x k turns x cells =
+        # 0.25 B x cells -- divided by the average launch duration (HIP events on the
+        # engine's stream over the timed region / launches, inter-kernel gaps included).
+        # `traffic` = the PMC-measured HBM bytes per launch of the same kernel (profiles/).
+        # The k = 1 equivalent (0.25 B per cell-update x all cell-updates) is reported
+        # separately: it exceeds the HBM peak once k > 1, so it is not a fraction of a roof.
+        cells_local = m["rows_local"] * W
+        launch_us = m["gpu_ms"] * 1e3 / max(m["launches"], 1)
+        turns_per_launch = a.steps / max(m["launches"], 1)
+        bytes_board = BYTES_PER_CELL_UPDATE * cells_local
+        bytes_k1 = BYTES_PER_CELL_UPDATE * turns_per_launch * cells_local
+        achieved = bytes_board / (launch_us * 1e-6) / 1e9
+        traffic, traffic_src = pmc_traffic(W, K)
         out = {
             "metric": METRIC,
             "value": round(gcups, 2),
@@ -217,36 +263,38 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": round(wall * 1e3 / a.steps, 5),
+            "ms_per_step": round(m["wall"] * 1e3 / a.steps, 5),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": f"{W}x{H} random torus board (seed {a.seed}), "
-                                   f"{a.steps} turns, bit-packed stencil, {K} turns per launch",
+                                   f"{a.steps} turns, bit-packed stencil, up to {K} turns "
+                                   f"per launch",
                        "board": [W, H], "turns": a.steps,
-                       "parallelism": f"row-strips x{world}" + (
-                           f", halo {info.halo}, "
-                           + ({"rccl": "RCCL send/recv on the engine stream",
-                               "torch": "RCCL via torch batch_isend_irecv"}[a.transport]
-                              if a.backend == "nccl" else "gloo host-staged")
-                           if world > 1 else ""),
-                       "band_rows": info.band_rows, "fast_path": bool(info.fast_path),
+                       "parallelism": parallelism(a, world, m),
+                       "band_rows": m["band"], "fast_path": m["fast"],
                        "temporal_blocking_k": K},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "definition": f"k=1 bytes (SURVEY 8d): 0.25 B per cell-update x "
-                                       f"{turns_per_launch:g} turns x cells per launch",
+                         "definition": f"algorithmic HBM bytes of one blocked launch: 0.25/k B "
+                                       f"per cell-update x k turns x cells = one read + one "
+                                       f"write of the packed board ({int(bytes_board)} B), k = "
+                                       f"{turns_per_launch:g} turns per launch on average, per "
+                                       f"average launch time",
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": f"k_step_skew<K={K}> (interleaved layout)" if K > 1
                                    else "k_step_ring<D=3>",
-                         "launch_us": round(launch_us, 2), "launches": launches,
+                         "launch_us": round(launch_us, 2), "launches": m["launches"],
                          "turns_per_launch": round(turns_per_launch, 3),
-                         "bytes_per_launch": int(bytes_k1),
-                         "board_bytes_per_launch": int(bytes_board),
-                         "board_achieved": round(board_achieved, 1),
-                         "board_frac": round(board_achieved / HBM_PEAK_GBS, 4)},
+                         "bytes_per_launch": int(bytes_board)},
+            "k1_equivalent": {"achieved": round(bytes_k1 / (launch_us * 1e-6) / 1e9, 1),
+                              "unit": "GB/s",
+                              "definition": "0.25 B per cell-update (SURVEY 8d, k = 1) x every "
+                                            "cell-update of a launch, per launch time: the HBM "
+                                            "bandwidth a one-turn-per-pass kernel would need "
+                                            "to match this rate"},
             "valu_roofline": None,
             "cpu_baseline": None,
         }
@@ -258,12 +306,23 @@ def main():
                 "model": "52 SIMD cycles per 4096 cell-updates (18 full-rate v_bitop3 + 4 "
                          "half-rate v_alignbit/DPP), 1024 SIMDs x 2.4 GHz; useful cell-updates "
                          "only (halo lanes, band halos and pipeline fill count against it)"}
+        if c3 is not None:
+            g3 = c3["W"] * c3["H"] * c3["steps"] / c3["wall"] / 1e9
+            l3 = c3["gpu_ms"] * 1e3 / max(c3["launches"], 1)
+            b3 = BYTES_PER_CELL_UPDATE * c3["rows_local"] * c3["W"]
+            out["configs_measured"] = [{
+                "workload": f"{c3['W']}x{c3['H']} random torus board (seed {a.seed}), "
+                            f"{c3['steps']} turns (BASELINE configs[2])",
+                "value": round(g3, 2), "unit": "GCUPS", "n_gpus": world,
+                "ms_per_step": round(c3["wall"] * 1e3 / c3["steps"], 5),
+                "parallelism": parallelism(a, world, c3),
+                "band_rows": c3["band"], "temporal_blocking_k": c3["K"],
+                "launch_us": round(l3, 2), "launches": c3["launches"],
+                "roofline_frac": round(b3 / (l3 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "valu_roofline_frac": round(g3 / world / VALU_PEAK_GCUPS, 4)}]
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(W, a.seed, a.cpu_turns, a.cpu_cores)
         print(json.dumps(out), flush=True)
-    if world > 1 and getattr(runner, "rccl", None) is not None:
-        runner.rccl.close()
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -17,12 +17,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gol_amd.h"
@@ -63,9 +65,18 @@ struct gol_ctx {
     size_t staging_size = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;              // boundary-band launches of gol_step_overlap
+    hipEvent_t ev_side = nullptr, ev_main = nullptr;
     long long turn = 0;
     long long launches = 0;
     int halo_valid = 0;
+    bool blocking_limited = false;           // temporal blocking off: buffer >= 2 GiB
+    // control word (gol_set_control): read by gol_step between launches, written by any
+    // thread without the engine lock (the reference's CFput flag channel)
+    std::atomic<int> control{GOL_CONTROL_RUN};
+    std::atomic<bool> control_used{false};
+    std::atomic<long long> progress{0};      // lock-free mirror of `turn` (gol_get_progress)
+    std::atomic<bool> parked{false};         // gol_step is parked on GOL_CONTROL_PAUSE
     std::string err;
     std::recursive_mutex mu;
 };
@@ -145,6 +156,29 @@ int ensure_layout(gol_ctx *c, bool il)
     c->cur ^= 1;
     c->il = il;
     return GOL_OK;
+}
+
+// Turns fused into the next launch when `room` turns remain before the next sync point
+// (end of the gol_step call, or the next halo exchange of a strip engine).  The turns are
+// spread over ceil(room / tpl) launches of near-equal depth: a short tail launch costs
+// almost as much as a full one (K=2: 29 us vs K=6: 37 us on an 8448-row strip), so 128
+// turns at tpl 6 run as 18 x 6 + 4 x 5, not 21 x 6 + 2.  1 = the one-turn kernel.
+// gol_step and gol_halo_buffers both use this rule (the zero-copy halo layout must be
+// the layout the first launch after an exchange runs on).
+int launch_depth(const gol_ctx *c, int64_t room)
+{
+    if (c->tpl <= 1 || room < 2 || (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) ||
+        c->blocked_pending)
+        return 1;
+    const int64_t nl = (room + c->tpl - 1) / c->tpl;
+    const int k = (int)((room + nl - 1) / nl);
+    return golk::multi_ok(c->cfg.width, k) ? k : 1;
+}
+
+// the word layout a launch of depth k runs on
+bool stepping_il(const gol_ctx *c, int k)
+{
+    return k > 1 && golk::multi_is_il(c->multi_words, c->multi_variant);
 }
 
 // popcount of owned rows of the current board -> *alive (synchronous)
@@ -351,7 +385,9 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 8 : 6);
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
     c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
-    if (!c->fast || !golk::multi_fits(c->nw, c->pitch, c->buf_rows)) c->tpl = 1;
+    if (c->fast && c->tpl > 1 && !golk::multi_fits(c->nw, c->pitch, c->buf_rows))
+        c->blocking_limited = true;   // reported in gol_info.blocking_limited
+    if (!c->fast || c->blocking_limited) c->tpl = 1;
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);
@@ -375,7 +411,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         (e = hipMalloc(&c->board[1], words * 8)) != hipSuccess ||
         (e = hipMalloc(&c->counts, (size_t)(kRing + 1) * kShards * 8)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_counts, kShards * 8, hipHostMallocDefault)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess) {
+        (e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming)) != hipSuccess) {
         rc = e == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP;
         return bail(rc);
     }
@@ -401,6 +440,7 @@ void gol_destroy(gol_ctx *c)
         DeviceGuard g(c->device);
         if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
         if (c->stream && c->stream != c->own_stream) (void)hipStreamSynchronize(c->stream);
+        if (c->side) (void)hipStreamSynchronize(c->side);
         if (c->board[0]) (void)hipFree(c->board[0]);
         if (c->board[1]) (void)hipFree(c->board[1]);
         if (c->blocked) (void)hipFree(c->blocked);
@@ -408,6 +448,9 @@ void gol_destroy(gol_ctx *c)
         if (c->staging) (void)hipFree(c->staging);
         if (c->h_counts) (void)hipHostFree(c->h_counts);
         if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+        if (c->side) (void)hipStreamDestroy(c->side);
+        if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+        if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     }
     delete c;
 }
@@ -432,6 +475,7 @@ int gol_get_info(gol_ctx *c, gol_info *info)
     info->turn = c->turn;
     info->nonbinary_cells = c->nonbinary;
     info->launches = c->launches;
+    info->blocking_limited = c->blocking_limited ? 1 : 0;
     return GOL_OK;
 }
 
@@ -489,6 +533,7 @@ int gol_load(gol_ctx *c, const uint8_t *bytes)
     c->cur = 0;
     c->il = false;
     c->turn = 0;
+    c->progress.store(0);
     c->launches = 0;
     c->halo_valid = c->cfg.halo;
     c->raw_turn0.clear();
@@ -517,6 +562,7 @@ int gol_load_packed(gol_ctx *c, const uint64_t *words)
     c->cur = 0;
     c->il = false;
     c->turn = 0;
+    c->progress.store(0);
     c->launches = 0;
     c->nonbinary = 0;
     c->raw_turn0.clear();
@@ -537,6 +583,7 @@ int gol_fill_random(gol_ctx *c, uint64_t seed)
     c->cur = 0;
     c->il = false;
     c->turn = 0;
+    c->progress.store(0);
     c->launches = 0;
     c->nonbinary = 0;
     c->raw_turn0.clear();
@@ -544,10 +591,17 @@ int gol_fill_random(gol_ctx *c, uint64_t seed)
     return GOL_OK;
 }
 
-int gol_step(gol_ctx *c, int64_t turns)
+namespace {
+
+constexpr int kCtlDepth = 2;   // launches queued ahead while a control word is in use
+
+// gol_step / gol_step_overlap.  xstream != null: the first launch is split -- the rows
+// whose k-turn dependency cone stays inside the owned rows run on the engine stream at
+// once, the rows next to the halos run on the side stream after everything queued on
+// xstream (the caller's halo receives) -- and the engine stream joins the side stream
+// before the next launch.
+int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
 {
-    if (!c || turns < 0) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
     if (is_strip(c) && turns > c->halo_valid)
         return fail(c, GOL_ESTATE, "strip engine: %lld turns requested, halos valid for %d",
                     (long long)turns, c->halo_valid);
@@ -564,20 +618,35 @@ int gol_step(gol_ctx *c, int64_t turns)
     a.variant = c->variant;
     a.multi_words = c->multi_words;
     a.multi_variant = c->multi_variant;
-    for (int64_t t = 0; t < turns;) {
-        // temporal blocking: fuse k turns into one pass when nothing needs per-turn output
-        int k = 1;
-        if (c->tpl > 1 && !cnt && !c->blocked_pending) {
-            int64_t room = turns - t;
-            if (is_strip(c)) room = std::min<int64_t>(room, c->halo_valid);
-            // spread the turns left before the next sync point over ceil(room / tpl)
-            // launches of near-equal depth: a short tail launch costs almost as much as a
-            // full one (K=2: 29 us vs K=6: 37 us on an 8448-row strip), so 128 turns at
-            // tpl 6 run as 18 x 6 + 4 x 5, not 21 x 6 + 2
-            const int64_t nl = (room + c->tpl - 1) / c->tpl;
-            k = (int)((room + nl - 1) / nl);
-            if (!golk::multi_ok(c->cfg.width, k)) k = 1;
+    // control word: with a controlling thread present, keep at most kCtlDepth launches
+    // queued so a pause / stop takes effect within that many launches
+    struct EventRing {
+        hipEvent_t ev[kCtlDepth] = {};
+        int n = 0;
+        ~EventRing()
+        {
+            for (int i = 0; i < std::min(n, kCtlDepth); ++i) (void)hipEventDestroy(ev[i]);
         }
+    } ring;
+    const bool ctl = c->control_used.load();
+    for (int64_t t = 0; t < turns;) {
+        if (ctl) {
+            int w = c->control.load();
+            if (w == GOL_CONTROL_PAUSE) {
+                // park at this launch boundary with the board complete (Server/gol/
+                // distributor.go:147-156: the turn loop blocks until the second 'p')
+                HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+                c->parked.store(true);
+                while ((w = c->control.load()) == GOL_CONTROL_PAUSE)
+                    std::this_thread::sleep_for(std::chrono::microseconds(200));
+                c->parked.store(false);
+            }
+            if (w == GOL_CONTROL_STOP)   // quit / kill (distributor.go:143-146,157-164)
+                return GOL_STOPPED;
+        }
+        int64_t room = turns - t;
+        if (is_strip(c)) room = std::min<int64_t>(room, c->halo_valid);
+        const int k = launch_depth(c, room);
         // rows computed: torus -> all; strip -> [s, buf_rows - s) after turn s since exchange
         const int s0 = is_strip(c) ? c->cfg.halo - c->halo_valid : 0;
         if (is_strip(c)) {
@@ -587,19 +656,64 @@ int gol_step(gol_ctx *c, int64_t turns)
             a.row_lo = 0;
             a.row_hi = c->buf_rows;
         }
-        {
-            const int rc = ensure_layout(c, k > 1 && golk::multi_is_il(c->multi_words,
-                                                                        c->multi_variant));
-            if (rc) return rc;
-        }
+        if (int rc = ensure_layout(c, stepping_il(c, k))) return rc;
         a.in = c->board[c->cur];
         a.out = c->board[c->cur ^ 1];
+        // split this launch around the incoming halos (first launch of an overlapped step;
+        // with per-turn counts the launch waits for the receives whole instead)
+        const bool split = xstream && t == 0 && is_strip(c) && !cnt;
+        if (xstream && t == 0 && !split) {
+            HIP_OR_FAIL(c, hipEventRecord(c->ev_side, xstream));
+            HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_side, 0));
+        }
+        const int H = c->cfg.halo;
+        const int in_lo = H + k, in_hi = H + c->cfg.rows - k;   // interior output rows
+        if (split) {
+            // side stream: after the caller's receives (and the engine's queued work)
+            HIP_OR_FAIL(c, hipEventRecord(c->ev_main, c->stream));
+            HIP_OR_FAIL(c, hipStreamWaitEvent(c->side, c->ev_main, 0));
+            HIP_OR_FAIL(c, hipEventRecord(c->ev_side, xstream));
+            HIP_OR_FAIL(c, hipStreamWaitEvent(c->side, c->ev_side, 0));
+        }
         if (k > 1) {
             a.blocked = nullptr;
             a.counts = nullptr;
             a.band = c->band_multi;
-            HIP_OR_FAIL(c, golk::launch_step_multi(a, k, c->stream));
+            if (split && in_lo < in_hi) {
+                golk::StepArgs b = a;
+                b.row_lo = in_lo;
+                b.row_hi = in_hi;
+                HIP_OR_FAIL(c, golk::launch_step_multi(b, k, c->stream));
+                // boundary rows: short bands so the few rows still spread over many waves
+                b.band = std::min(c->band_multi, golk::kOverlapBand);
+                b.row_lo = a.row_lo;
+                b.row_hi = in_lo;
+                HIP_OR_FAIL(c, golk::launch_step_multi(b, k, c->side));
+                b.row_lo = in_hi;
+                b.row_hi = a.row_hi;
+                HIP_OR_FAIL(c, golk::launch_step_multi(b, k, c->side));
+            } else {
+                HIP_OR_FAIL(c, golk::launch_step_multi(a, k, split ? c->side : c->stream));
+            }
             a.band = c->band;
+        } else if (split) {
+            // one-turn launches: interior now, the 2 x (halo) boundary rows after the receives
+            a.blocked = c->blocked_pending ? c->blocked : nullptr;
+            a.counts = nullptr;
+            golk::StepArgs b = a;
+            if (in_lo < in_hi) {
+                b.row_lo = in_lo;
+                b.row_hi = in_hi;
+                HIP_OR_FAIL(c, golk::launch_step(b, c->fast, c->stream));
+                b.row_lo = a.row_lo;
+                b.row_hi = in_lo;
+                HIP_OR_FAIL(c, golk::launch_step(b, c->fast, c->side));
+                b.row_lo = in_hi;
+                b.row_hi = a.row_hi;
+                HIP_OR_FAIL(c, golk::launch_step(b, c->fast, c->side));
+            } else {
+                HIP_OR_FAIL(c, golk::launch_step(a, c->fast, c->side));
+            }
         } else {
             a.blocked = c->blocked_pending ? c->blocked : nullptr;
             a.counts = nullptr;
@@ -617,8 +731,13 @@ int gol_step(gol_ctx *c, int64_t turns)
             }
             HIP_OR_FAIL(c, golk::launch_step(a, c->fast, c->stream));
         }
+        if (split) {   // join: the next launch overwrites rows the side launches read
+            HIP_OR_FAIL(c, hipEventRecord(c->ev_side, c->side));
+            HIP_OR_FAIL(c, hipStreamWaitEvent(c->stream, c->ev_side, 0));
+        }
         c->cur ^= 1;
         c->turn += k;
+        c->progress.store(c->turn);
         c->launches += 1;
         t += k;
         if (is_strip(c)) c->halo_valid -= k;
@@ -627,11 +746,62 @@ int gol_step(gol_ctx *c, int64_t turns)
             c->blocked_pending = false;
             c->raw_turn0.clear();
         }
+        if (ctl) {   // bound the queue: wait for the launch kCtlDepth back
+            hipEvent_t &e = ring.ev[ring.n % kCtlDepth];
+            if (ring.n >= kCtlDepth) HIP_OR_FAIL(c, hipEventSynchronize(e));
+            else HIP_OR_FAIL(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIP_OR_FAIL(c, hipEventRecord(e, c->stream));
+            ++ring.n;
+        }
     }
     if (c->blocked && !c->blocked_pending) {
         HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
         release_blocked(c);
     }
+    return GOL_OK;
+}
+
+}  // namespace
+
+int gol_step(gol_ctx *c, int64_t turns)
+{
+    if (!c || turns < 0) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    return step_impl(c, turns, nullptr);
+}
+
+int gol_step_overlap(gol_ctx *c, int64_t turns, void *recv_stream)
+{
+    if (!c || turns < 0 || !recv_stream) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!is_strip(c)) return fail(c, GOL_ESTATE, "not a strip engine");
+    c->halo_valid = c->cfg.halo;   // the receives queued on recv_stream refresh the halos
+    return step_impl(c, turns, (hipStream_t)recv_stream);
+}
+
+int gol_stream_wait(gol_ctx *c, void *stream)
+{
+    if (!c || !stream) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    HIP_OR_FAIL(c, hipEventRecord(c->ev_main, c->stream));
+    HIP_OR_FAIL(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_main, 0));
+    return GOL_OK;
+}
+
+int gol_set_control(gol_ctx *c, int32_t word)
+{
+    if (!c || word < GOL_CONTROL_RUN || word > GOL_CONTROL_STOP) return GOL_EINVAL;
+    c->control_used.store(true);
+    c->control.store(word);
+    return GOL_OK;
+}
+
+int gol_get_progress(gol_ctx *c, int64_t *turn, int32_t *parked)
+{
+    if (!c) return GOL_EINVAL;
+    if (turn) *turn = c->progress.load();
+    if (parked) *parked = c->parked.load() ? 1 : 0;
     return GOL_OK;
 }
 
@@ -919,14 +1089,12 @@ int gol_halo_buffers(gol_ctx *c, void **send_top, void **send_bottom, void **rec
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     if (!is_strip(c)) return fail(c, GOL_ESTATE, "not a strip engine");
     DeviceGuard g(c->device);
-    // the layout the first launch after a full exchange runs on (gol_step's rule at
-    // halo_valid == halo): a function of width, halo and flags only, so equal on every rank
-    bool il = false;
-    if (c->tpl > 1 && !(c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) && !c->blocked_pending) {
-        int k = std::min(c->cfg.halo, c->tpl);
-        if (k == 7) k = 6;
-        il = golk::multi_ok(c->cfg.width, k) && golk::multi_is_il(c->multi_words, c->multi_variant);
-    }
+    // the layout the first launch after a full exchange runs on: gol_step's own rule
+    // (launch_depth) with halo turns to go -- whatever the step after the exchange asks
+    // for, its first launch has depth launch_depth(min(turns, halo)); the layout is the
+    // same for every depth >= 2, and a function of width, halo and flags only, so equal
+    // on every rank
+    const bool il = stepping_il(c, launch_depth(c, c->cfg.halo));
     if (int rc = ensure_layout(c, il)) return rc;
     uint64_t *b = c->board[c->cur];
     const int K = c->cfg.halo;

@@ -62,6 +62,8 @@ bool fast_path_ok(int width);
 // turns, reading rows [row_lo - turns, row_hi + turns) (mod modrows).  No blocked mask,
 // no counts.  turns in {2, 3, 4, 5, 6, 8}.
 constexpr int kMaxTurnsPerLaunch = 8;
+// band height of the boundary launches of an overlapped step (rows next to the halos)
+constexpr int kOverlapBand = 16;
 bool multi_ok(int width, int turns);
 bool multi_fits(int nw, int pitch, int rows);   // buffer < 2 GiB (k_step_skew buffer ranges)
 // the temporal-blocking kernel for (words per lane, variant) runs on the interleaved layout

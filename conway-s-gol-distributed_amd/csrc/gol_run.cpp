@@ -11,8 +11,9 @@
 //     process-global `turn` that is never reset: Server/gol/distributor.go:30,133);
 //   * TurnComplete{t} is emitted for every turn when enabled (event.go:55-60
 //     contract; the reference emits none: Local/gol/distributor.go:184-185);
-//   * control keys are sampled at chunk boundaries (a chunk is a few ms of GPU
-//     work) instead of after every single turn;
+//   * control keys are sampled at kernel-launch boundaries (a launch fuses up to
+//     turns_per_launch turns; multi-strip runs: chunk boundaries of a few ms) instead
+//     of after every single turn;
 //   * boards need not be square (the reference reads H x H bytes:
 //     Local/gol/distributor.go:80).
 #include <hip/hip_runtime.h>
@@ -190,6 +191,22 @@ struct gol_run {
     std::shared_ptr<std::vector<int64_t>> last_final;
     std::string error;
 
+    // single-engine runs: a key press interrupts the running chunk through the engine's
+    // control word (gol_set_control), so keys take effect within 2 kernel launches
+    std::mutex ctl_mu;
+    gol_ctx *ctl_engine = nullptr;
+    void interrupt()
+    {
+        std::lock_guard<std::mutex> lk(ctl_mu);
+        if (ctl_engine) (void)gol_set_control(ctl_engine, GOL_CONTROL_STOP);
+    }
+    void set_ctl_engine(gol_ctx *e)
+    {
+        std::lock_guard<std::mutex> lk(ctl_mu);
+        ctl_engine = e;
+        if (e) (void)gol_set_control(e, GOL_CONTROL_RUN);
+    }
+
     // ----------------------------------------------------------- channel
     bool send(const gol_event &ev, std::shared_ptr<std::vector<int64_t>> cells = nullptr)
     {
@@ -365,12 +382,15 @@ struct Strips {
         return GOL_OK;
     }
 
-    // advance `turns` turns (asynchronous on the engines' streams)
+    long long engine_turn() { return golint::engine_turn(eng[0]); }
+
+    // advance `turns` turns (asynchronous on the engines' streams); a single engine stops
+    // early when its control word says so (engine_turn() tells how far it got)
     int step(long long turns)
     {
         if (!strip_mode()) {
             int rc = gol_step(eng[0], turns);
-            return rc ? fail_from(eng[0], rc) : GOL_OK;
+            return rc < 0 ? fail_from(eng[0], rc) : GOL_OK;
         }
         while (turns > 0) {
             int hv = halo_valid();
@@ -545,8 +565,15 @@ void gol_run::run()
 
     long long chunk = 1;
     bool quit = false, killed = false;
+    struct CtlScope {   // the key thread may interrupt this run's engine while it lives
+        gol_run *r;
+        CtlScope(gol_run *r_, gol_ctx *e) : r(r_) { r->set_ctl_engine(e); }
+        ~CtlScope() { r->set_ctl_engine(nullptr); }
+    } ctl_scope(this, st.strip_mode() ? nullptr : st.eng[0]);
     while (turn < p.turns && !quit) {
         if (abort.load()) return close();
+        // re-arm before draining the keys: a key pushed from here on stops the next chunk
+        if (!st.strip_mode()) (void)gol_set_control(st.eng[0], GOL_CONTROL_RUN);
         int k;
         while (!quit && pop_key(k)) {
             if (k == 's') {                           // distributor.go:131-144
@@ -576,9 +603,11 @@ void gol_run::run()
         if (quit) break;
         if (!tick()) return close();
 
-        const long long n = std::min(chunk, p.turns - turn);
+        const long long want = std::min(chunk, p.turns - turn);
         const auto t0 = Clock::now();
-        if (st.step(n) || st.sync()) return die(st.err);
+        const long long before = st.engine_turn();
+        if (st.step(want) || st.sync()) return die(st.err);
+        const long long n = st.engine_turn() - before;   // < want if a key interrupted it
         const double ms =
             std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
         if (emit_cell_flipped) {
@@ -717,9 +746,12 @@ int64_t gol_run_final_alive(gol_run *r, int64_t *xy, int64_t cap)
 int gol_run_key(gol_run *r, int32_t rune)
 {
     if (!r) return GOL_EINVAL;
-    std::lock_guard<std::mutex> lk(r->kmu);
-    r->keys.push_back(rune);
-    r->kcv.notify_all();
+    {
+        std::lock_guard<std::mutex> lk(r->kmu);
+        r->keys.push_back(rune);
+        r->kcv.notify_all();
+    }
+    if (rune == 's' || rune == 'p' || rune == 'q' || rune == 'k') r->interrupt();
     return GOL_OK;
 }
 

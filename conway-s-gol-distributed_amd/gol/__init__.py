@@ -115,23 +115,32 @@ class FinalTurnComplete(Event):
 
 
 # ----------------------------------------------------------------- channel
+class RunError(RuntimeError):
+    """A run ended on an error (the reference panics: util.Check / log.Fatal,
+    Local/util/check.go:3-7, Server/gol/distributor.go:89-92)."""
+
+
 class Channel:
     """A Go-like channel: bounded FIFO (capacity 0 behaves as capacity 1),
-    ``close()``, ``recv() -> (value, ok)`` and iteration until closed+drained."""
+    ``close()``, ``recv() -> (value, ok)`` and iteration until closed+drained.
+    ``close(error)`` closes it with an error: once the queued values are drained,
+    ``recv`` and iteration raise ``RunError`` instead of reporting a clean close."""
 
     _CLOSED = object()
 
     def __init__(self, capacity: int = 0):
         self._q: queue.Queue = queue.Queue(maxsize=max(int(capacity), 1))
         self._closed = threading.Event()
+        self.error: Optional[str] = None
 
     def send(self, v):
         if self._closed.is_set():
             raise RuntimeError("send on closed channel")
         self._q.put(v)
 
-    def close(self):
+    def close(self, error: Optional[str] = None):
         if not self._closed.is_set():
+            self.error = error
             self._closed.set()
             self._q.put(Channel._CLOSED)
 
@@ -139,6 +148,8 @@ class Channel:
         v = self._q.get(timeout=timeout)
         if v is Channel._CLOSED:
             self._q.put(Channel._CLOSED)      # stay closed for other receivers
+            if self.error:
+                raise RunError(self.error)
             return None, False
         return v, True
 
@@ -176,8 +187,11 @@ class RunHandle:
                 self._L.gol_run_destroy(self._h)
 
     def wait(self, timeout: Optional[float] = None):
+        """Join the pump threads; raises RunError if the run failed."""
         for t in self.threads:
             t.join(timeout)
+        if self.error:
+            raise RunError(self.error)
 
 
 def _to_event(ev: N.gol_event, h, L, alive_as_array: bool):
@@ -219,6 +233,9 @@ def Run(p: Params, events: Channel, keyPresses: Optional[Channel] = None, *,
     reference's ``len(SUB)``), one engine each.  ``resume`` = the reference's
     ``CONT=yes`` (None: read the CONT environment variable).
     """
+    if devices is not None and len(devices) != int(ngpus):
+        # gol_run_start reads devices[0..ngpus-1]
+        raise ValueError(f"devices lists {len(devices)} ordinals for ngpus={ngpus}")
     L = N.lib()
     prm = N.gol_params(int(p.Turns), int(p.Threads), int(p.ImageWidth), int(p.ImageHeight))
     opts = N.gol_run_options()
@@ -250,13 +267,15 @@ def Run(p: Params, events: Channel, keyPresses: Optional[Channel] = None, *,
                     break
                 N.check(rc)
                 events.send(_to_event(ev, h, L, alive_as_array))
+        except Exception as e:              # a native error code while pumping
+            handle.error = str(e)
         finally:
             err = L.gol_run_error(h)
-            if err:
+            if err and not handle.error:
                 handle.error = err.decode()
             done.set()
             handle._destroy()
-            events.close()
+            events.close(handle.error)
 
     def keys():
         while not done.is_set():
@@ -281,7 +300,7 @@ def Run(p: Params, events: Channel, keyPresses: Optional[Channel] = None, *,
 
 
 __all__ = [
-    "Params", "Run", "RunHandle", "Channel", "Cell", "State", "Event", "AliveCellsCount",
+    "Params", "Run", "RunHandle", "RunError", "Channel", "Cell", "State", "Event", "AliveCellsCount",
     "ImageOutputComplete", "StateChange", "CellFlipped", "TurnComplete", "FinalTurnComplete",
     "Engine", "strip_split", "haloed_rows",
 ]

@@ -24,6 +24,11 @@ GOL_ENODEV = -5
 GOL_EIO = -6
 GOL_ECLOSED = -7
 GOL_ETIMEDOUT = -8
+GOL_STOPPED = 1
+
+GOL_CONTROL_RUN = 0
+GOL_CONTROL_PAUSE = 1
+GOL_CONTROL_STOP = 2
 
 GOL_FLAG_COUNT_EVERY_TURN = 0x1
 GOL_FLAG_FORCE_GENERIC = 0x2
@@ -60,7 +65,7 @@ class gol_info(ctypes.Structure):
                 ("halo_valid", ctypes.c_int32), ("turns_per_launch", ctypes.c_int32),
                 ("device", ctypes.c_int32),
                 ("turn", ctypes.c_int64), ("nonbinary_cells", ctypes.c_int64),
-                ("launches", ctypes.c_int64)]
+                ("launches", ctypes.c_int64), ("blocking_limited", ctypes.c_int32)]
 
 
 class gol_params(ctypes.Structure):
@@ -108,6 +113,10 @@ SIGNATURES = {
     "gol_fill_random": (_i32, [_vp, ctypes.c_uint64]),
     "gol_load_packed": (_i32, [_vp, _u64p]),
     "gol_step": (_i32, [_vp, _i64]),
+    "gol_set_control": (_i32, [_vp, _i32]),
+    "gol_get_progress": (_i32, [_vp, _i64p, ctypes.POINTER(ctypes.c_int32)]),
+    "gol_stream_wait": (_i32, [_vp, _vp]),
+    "gol_step_overlap": (_i32, [_vp, _i64, _vp]),
     "gol_snapshot": (_i32, [_vp, _i64p, _i64p]),
     "gol_turn_counts": (_i32, [_vp, _i64, _i64, _i64p]),
     "gol_read_board": (_i32, [_vp, _u8p]),

@@ -75,6 +75,10 @@ class EngineStrip:
         self._views = None                     # board pointers move with every step
         self.engine.step(n)
 
+    def step_overlap(self, n: int, recv_stream_ptr: int):
+        self._views = None
+        self.engine.step_overlap(n, recv_stream_ptr)
+
     def stream_context(self):
         return torch.cuda.stream(self.stream)
 
@@ -120,12 +124,18 @@ class DistStrip:
     """One rank's strip; ``step(turns)`` interleaves local turns and halo exchanges."""
 
     def __init__(self, strip, rank: int, world: int, group=None, stage_on_host: bool = False,
-                 rccl=None):
+                 rccl=None, overlap: bool = False):
         """``rccl``: a gol.rccl.RcclComm -- the exchange is enqueued by direct RCCL calls on
         the strip's own stream (no cross-stream waits); None = torch.distributed
-        point-to-point (batch_isend_irecv on the nccl backend, isend/irecv on gloo)."""
+        point-to-point (batch_isend_irecv on the nccl backend, isend/irecv on gloo).
+        ``overlap`` (direct RCCL, zero-copy strips only): the sends and receives run on a
+        stream of their own while the first launch's interior rows compute
+        (gol_stream_wait / gol_step_overlap); the rows next to the halos follow the
+        receives."""
         self.strip = strip
         self.rccl = rccl
+        self.overlap = bool(overlap and rccl is not None and getattr(strip, "zero_copy", False))
+        self.comm_stream = torch.cuda.Stream(strip.device) if self.overlap else None
         self.rank, self.world = int(rank), int(world)
         self.up = (self.rank - 1) % self.world
         self.down = (self.rank + 1) % self.world
@@ -189,10 +199,32 @@ class DistStrip:
         self.strip.import_rows(top_recv, bot_recv)
         self.exchanges += 1
 
+    def _exchange_overlapped(self, turns: int):
+        """Exchange on the comm stream and advance `turns` (<= halo) turns, the first
+        launch's interior rows concurrently with the transfer."""
+        top, bot = self.strip.export_rows()
+        top_recv, bot_recv = self.strip.recv_buffers()
+        if not self._layout_checked:
+            self._check_layout(top)
+        eng = self.strip.engine
+        cs = self.comm_stream.cuda_stream
+        eng.stream_wait(cs)                     # the send rows are final
+        nbytes = top.numel() * top.element_size()
+        self.rccl.exchange([(top.data_ptr(), self.up), (bot.data_ptr(), self.down)],
+                           [(bot_recv.data_ptr(), self.down), (top_recv.data_ptr(), self.up)],
+                           nbytes, cs)
+        self.strip.step_overlap(turns, cs)
+        self.exchanges += 1
+
     def step(self, turns: int):
         turns = int(turns)
         while turns > 0:
             if self.strip.halo_valid == 0:
+                if self.overlap:
+                    n = min(turns, self.strip.engine.halo)
+                    self._exchange_overlapped(n)
+                    turns -= n
+                    continue
                 self.exchange()
             n = min(turns, self.strip.halo_valid)
             self.strip.step(n)

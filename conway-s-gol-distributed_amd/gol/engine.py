@@ -108,8 +108,31 @@ class Engine:
     def fill_random(self, seed: int):
         self._c(self._L.gol_fill_random(self._h, ctypes.c_uint64(int(seed))))
 
-    def step(self, turns: int = 1):
-        self._c(self._L.gol_step(self._h, int(turns)))
+    def step(self, turns: int = 1) -> bool:
+        """Advance `turns` turns; False if the control word stopped it early."""
+        return self._c(self._L.gol_step(self._h, int(turns))) != N.GOL_STOPPED
+
+    # -- control word (reference CFput handshake, Server/gol/distributor.go:54-60,136-164)
+    def set_control(self, word: int):
+        """GOL_CONTROL_RUN / _PAUSE / _STOP; safe from any thread while step() runs."""
+        self._c(self._L.gol_set_control(self._h, int(word)))
+
+    def progress(self):
+        """Lock-free (turns enqueued so far, parked on PAUSE)."""
+        t, p = ctypes.c_int64(), ctypes.c_int32()
+        self._c(self._L.gol_get_progress(self._h, ctypes.byref(t), ctypes.byref(p)))
+        return int(t.value), bool(p.value)
+
+    # -- overlapped halo exchange (gol_stream_wait / gol_step_overlap)
+    def stream_wait(self, stream_ptr: int):
+        """Make `stream_ptr` wait for the work queued on the engine so far."""
+        self._c(self._L.gol_stream_wait(self._h, ctypes.c_void_p(int(stream_ptr))))
+
+    def step_overlap(self, turns: int, recv_stream_ptr: int):
+        """Mark the halos fresh and advance `turns` turns, the first launch's interior
+        rows at once and its boundary rows after the work queued on recv_stream_ptr."""
+        self._c(self._L.gol_step_overlap(self._h, int(turns),
+                                         ctypes.c_void_p(int(recv_stream_ptr))))
 
     def snapshot(self):
         """(completed turns, alive cells) — the reference's Alivecount pair."""

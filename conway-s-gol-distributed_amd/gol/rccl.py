@@ -75,20 +75,32 @@ class RcclComm:
     rank must create it, with its HIP device current)."""
 
     def __init__(self, rank: int, world: int, device: torch.device, group=None):
-        L = lib()
         self.rank, self.world = int(rank), int(world)
+        self.comm = ctypes.c_void_p()
         uid = _UniqueId()
-        if self.rank == 0:
-            _check(L.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        err = None
+        try:
+            L = lib()
+            if self.rank == 0:
+                _check(L.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        except (OSError, AttributeError, RuntimeError) as e:   # no library / symbol / uid
+            err = e
         if self.world > 1:
             on_dev = dist.get_backend(group) == "nccl"
+            where = device if on_dev else "cpu"
+            # every rank learns whether every rank has a library (and rank 0 a unique id)
+            # before anyone blocks in the broadcast or in ncclCommInitRank
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=where)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            if int(ok.item()) == 0:
+                raise RuntimeError(f"rank {self.rank}: direct RCCL unavailable on some rank"
+                                   + (f" ({err})" if err else ""))
             t = torch.frombuffer(bytearray(bytes(uid.internal).ljust(_UID_BYTES, b"\0")),
-                                 dtype=torch.uint8).clone()
-            if on_dev:
-                t = t.to(device)
+                                 dtype=torch.uint8).clone().to(where)
             dist.broadcast(t, src=0, group=group)
             uid.internal = bytes(t.cpu().tolist())
-        self.comm = ctypes.c_void_p()
+        elif err is not None:
+            raise RuntimeError(f"direct RCCL unavailable ({err})")
         with torch.cuda.device(device):
             _check(L.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),
                    "ncclCommInitRank")

@@ -54,6 +54,8 @@ extern "C" {
 #define GOL_EIO        -6   /* PGM file missing / malformed (reference: panic)       */
 #define GOL_ECLOSED    -7   /* run driver: event channel closed                      */
 #define GOL_ETIMEDOUT  -8   /* run driver: no event within the timeout               */
+#define GOL_STOPPED     1   /* gol_step returned early on GOL_CONTROL_STOP (not an error:
+                               the turns done so far are in gol_info.turn)            */
 
 /* ----------------------------------------------------------------- engine */
 typedef struct gol_ctx gol_ctx;
@@ -90,6 +92,9 @@ typedef struct gol_info {
     int64_t  turn;              /* completed turns since load                          */
     int64_t  nonbinary_cells;   /* cells that were neither 0 nor 255 at load           */
     int64_t  launches;          /* stencil kernel launches since load                  */
+    int32_t  blocking_limited;  /* 1 = temporal blocking is off because a board buffer is
+                                   >= 2 GiB (the multi-turn kernel's 32-bit buffer offsets):
+                                   every launch runs one turn                          */
 } gol_info;
 
 /* Whole-board (torus) engine on the current device. */
@@ -124,8 +129,38 @@ int gol_fill_random(gol_ctx *ctx, uint64_t seed);
 int gol_load_packed(gol_ctx *ctx, const uint64_t *words);
 
 /* Advance `turns` turns.  Torus engine: any turns >= 0.  Strip engine:
- * turns <= halo_valid (then exchange halos; see gol_export_halo). */
+ * turns <= halo_valid (then exchange halos; see gol_export_halo).  Returns GOL_OK, or
+ * GOL_STOPPED when the control word (below) said stop between two launches. */
 int gol_step(gol_ctx *ctx, int64_t turns);
+
+/* Control word, the engine-level mirror of the reference's CFput flag handshake
+ * (Server/gol/distributor.go:54-60,136-164): any thread may set it at any time, without
+ * the engine lock.  gol_step reads it before every kernel launch (a launch fuses up to
+ * turns_per_launch turns): RUN continues, PAUSE parks gol_step at that launch boundary
+ * with the board complete until the word changes, STOP makes gol_step return GOL_STOPPED.
+ * Once an engine has seen gol_set_control, gol_step keeps at most 2 launches queued so
+ * the word takes effect within 2 launches.  The word stays set until changed. */
+#define GOL_CONTROL_RUN    0
+#define GOL_CONTROL_PAUSE  1
+#define GOL_CONTROL_STOP   2
+int gol_set_control(gol_ctx *ctx, int32_t word);
+/* Lock-free progress read for a controlling thread: *turn = turns enqueued so far (the
+ * board reaches it at the next gol_sync), *parked = 1 while gol_step is parked on PAUSE
+ * (the board is then complete at *turn).  Either pointer may be NULL. */
+int gol_get_progress(gol_ctx *ctx, int64_t *turn, int32_t *parked);
+
+/* Halo exchange overlapped with compute (strip engines; the zero-copy path of
+ * gol_halo_buffers).  gol_stream_wait makes `hip_stream` (the transport's stream) wait for
+ * the work queued on the engine so far -- the send rows are final.  The caller then
+ * enqueues its sends and receives on that stream and calls gol_step_overlap, which marks
+ * the halos fresh and advances `turns` (<= halo) turns: the first launch's interior rows
+ * (those whose dependency cone stays inside the owned rows) start on the engine stream at
+ * once, the rows next to the halos run on a second engine stream after the work queued on
+ * `recv_stream`, and the engine stream joins it before the next launch.  Replaces the
+ * reference's blocking fan-out / gather of every strip every turn
+ * (Server/gol/distributor.go:118-129). */
+int gol_stream_wait(gol_ctx *ctx, void *hip_stream);
+int gol_step_overlap(gol_ctx *ctx, int64_t turns, void *recv_stream);
 
 /* Consistent (turn, alive) pair of the current board (owned rows only). */
 int gol_snapshot(gol_ctx *ctx, int64_t *turn, int64_t *alive);
@@ -202,7 +237,8 @@ typedef struct gol_run_options {
     const char *image_dir;           /* where {W}x{H}.pgm is read ("images")            */
     const char *out_dir;             /* where {W}x{H}x{T}.pgm is written ("out")        */
     int32_t ngpus;                   /* row strips = engines (the reference's len(SUB)); 0 = 1 */
-    const int32_t *devices;          /* ngpus device ordinals, NULL = 0..ngpus-1 (mod device count) */
+    const int32_t *devices;          /* exactly ngpus device ordinals (the array is read at
+                                        indices 0..ngpus-1); NULL = 0..ngpus-1 (mod count)  */
     int32_t halo;                    /* strip halo depth K; 0 = auto                    */
     int32_t ticker_ms;               /* AliveCellsCount period; 0 = 2000 (distributor.go:58) */
     int32_t event_capacity;          /* bounded event channel; 0 = 1 (unbuffered-like)  */

@@ -50,6 +50,32 @@ def test_rccl_self_exchange(halo, tpl, copy, transport):
         assert f"layout={1 if tpl > 1 else 0}" in out
 
 
+@pytest.mark.parametrize("halo,tpl,height", [(8, 8, 640), (16, 8, 640), (5, 1, 640),
+                                             (6, 6, 640), (40, 8, 64), (40, 8, 12),
+                                             (128, 8, 300)])
+def test_rccl_self_exchange_overlapped(halo, tpl, height):
+    """The overlapped exchange (gol_stream_wait + direct RCCL on a stream of its own +
+    gol_step_overlap): the first launch after each exchange runs its interior rows at once
+    and the rows next to the halos after the receives.  Self-exchange at world size 1,
+    bit-exact against the oracle; the 12-row case has no interior rows at all, and
+    (128, 300) exchanges 128-row halos as the bench does."""
+    port = 29700 + halo + tpl
+    out = _dist_check(1, ["--backend", "nccl", "--halo", halo, "--tpl", tpl, "--height", height,
+                          "--transport", "rccl", "--overlap"], port)
+    assert "overlap=True" in out
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_rccl_self_exchange_65536(overlap):
+    """BASELINE C4 / C5 through the bench's own N > 1 path (DistStrip, direct RCCL, 128-row
+    halos, k-turn launches) at full size: 65536^2 seed 3, 1000 turns, world size 1 (the
+    rank is its own ring neighbour), against the oracle digest."""
+    out = _dist_check(1, ["--backend", "nccl", "--transport", "rccl", "--halo", 128, "--tpl", 0,
+                          "--digest", "65536x65536_seed3_t1000"] + (["--overlap"] if overlap else []),
+                      29800 + int(overlap))
+    assert "world=1 halo=128 exchanges=7" in out and f"overlap={overlap}" in out
+
+
 def test_halo_buffers_zero_copy_torus():
     """gol_halo_buffers: the four views are the strip's boundary and halo rows in the
     current board; copying send_bottom -> recv_top and send_top -> recv_bottom on the
@@ -99,7 +125,8 @@ def _bench_line(stdout):
 def test_bench_contract_one_gpu():
     """bench.py's single JSON line (driver contract) at a small size, CPU baseline included."""
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--size", "4096",
-                        "--steps", "64", "--warmup", "8", "--cpu-turns", "1"],
+                        "--steps", "64", "--warmup", "8", "--cpu-turns", "1",
+                        "--c3-size", "2048", "--c3-turns", "96"],
                        capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     d = _bench_line(p.stdout)
@@ -108,8 +135,13 @@ def test_bench_contract_one_gpu():
     assert d["n_gpus"] == 1 and d["steps"] == 64 and d["warmup"] == 8 and d["value"] > 0
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["peak"] == 8000.0 and r["launches"] >= 1
-    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
-    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["value"] > 0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and 0 < r["frac"] <= 1
+    assert d["k1_equivalent"]["achieved"] >= r["achieved"]
+    c3 = d["configs_measured"][0]
+    assert c3["value"] > 0 and "2048x2048" in c3["workload"]
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert f"{cb['cores']} OpenMP threads" in cb["sample"]
 
 
 def test_bench_torchrun_two_ranks_gloo():
@@ -118,7 +150,7 @@ def test_bench_torchrun_two_ranks_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", "--master-port=29611", os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--size", "4096", "--steps", "64", "--warmup", "8", "--halo", "16",
-           "--backend", "gloo"]
+           "--backend", "gloo", "--c3-size", "2048", "--c3-turns", "40"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert p.returncode == 0, p.stderr[-3000:]

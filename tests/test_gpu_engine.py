@@ -420,3 +420,81 @@ def test_65536_properties(gol, oracle):
         e.step(1)
         got = e.read_packed()
     assert np.array_equal(got, np.roll(np.roll(one, 1000, axis=0), 3, axis=1))
+
+
+# ------------------------------------------------- full-size strip forms (C4 / C5)
+@pytest.mark.parametrize("n", [4, 8])
+def test_65536_strips_in_process(gol, n):
+    """BASELINE configs C4 / C5 in strip form at full size on one GPU: 65536^2 seed 3 as
+    n row strips (the reference Server's split, Server/gol/distributor.go:106-116), each
+    its own engine with 128-row halos exchanged every 128 turns (temporal blocking inside:
+    k-turn launches, k-row shrinking trapezoids), 1000 turns, against the oracle digest."""
+    d = _digests()["65536x65536_seed3_t1000"]
+    w, h, turns, K = d["width"], d["height"], d["turns"], 128
+    parts = gol.strip_split(h, n)
+    engs = [gol.Engine(w, h, device=0, row_offset=o, rows=r, halo=K) for o, r in parts]
+    try:
+        for e in engs:
+            e.fill_random(d["seed"])            # global rows: the halos are the true rows
+        left = turns
+        while left:
+            if engs[0].halo_valid == 0:
+                for i, e in enumerate(engs):
+                    e.copy_halo_from_upper(engs[(i - 1) % n])
+                    e.copy_halo_from_lower(engs[(i + 1) % n])
+                for e in engs:
+                    e.halo_done()
+            m = min(left, engs[0].halo_valid)
+            for e in engs:
+                e.step(m)
+            left -= m
+        assert all(e.info().turns_per_launch > 1 for e in engs)
+        assert sum(e.snapshot()[1] for e in engs) == d["alive"]
+        hs = hashlib.sha256()
+        for e in engs:
+            hs.update(e.read_packed().tobytes())
+        assert hs.hexdigest() == d["sha256"]
+    finally:
+        for e in engs:
+            e.close()
+
+
+# ---------------------------------------------------------------- control word
+def test_control_word_pause_and_stop(gol, oracle):
+    """gol_set_control from a second thread while gol_step runs (the reference's CFput
+    flag handshake, Server/gol/distributor.go:54-60,136-164): PAUSE parks gol_step at a
+    launch boundary with the board complete, STOP makes it return early; the board is the
+    oracle's board at the reported turn."""
+    import threading
+    import time
+    from gol import _native as N
+    w = h = 512
+    with _engine(gol, w, h) as e:
+        e.fill_random(21)
+        e.set_control(N.GOL_CONTROL_RUN)
+        res = {}
+        th = threading.Thread(target=lambda: res.update(done=e.step(10 ** 9)), daemon=True)
+        th.start()
+        time.sleep(0.05)
+        e.set_control(N.GOL_CONTROL_PAUSE)
+        t_end = time.time() + 10
+        while not e.progress()[1] and time.time() < t_end:
+            time.sleep(0.001)
+        t_paused, parked = e.progress()
+        assert parked and t_paused > 0
+        time.sleep(0.05)
+        assert e.progress() == (t_paused, True)      # parked: no launch in between
+        e.set_control(N.GOL_CONTROL_STOP)
+        th.join(10)
+        assert not th.is_alive() and res["done"] is False
+        e.sync()
+        assert e.turn == t_paused and e.progress() == (t_paused, False)
+        got = e.read_packed()
+        # STOP persists until changed: a step returns at once, RUN resumes
+        assert e.step(5) is False and e.turn == t_paused
+        e.set_control(N.GOL_CONTROL_RUN)
+        assert e.step(7) is True and e.turn == t_paused + 7
+        after = e.read_packed()
+    want = oracle.bit_run(oracle.gen_random(21, w, h), w, t_paused)
+    assert np.array_equal(got, want)
+    assert np.array_equal(after, oracle.bit_run(want, w, 7))

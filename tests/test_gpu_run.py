@@ -180,8 +180,12 @@ def test_missing_image_reports_error(gol, workdir):
     events = gol.Channel()
     h = gol.Run(p, events, None, image_dir=str(workdir / "images"),
                 out_dir=str(workdir / "out"))
-    assert list(events) == []
-    h.wait(5)
+    # the reference panics (util.Check); here the channel closes with the error and both
+    # iteration and wait() raise it
+    with pytest.raises(gol.RunError, match="32x32"):
+        list(events)
+    with pytest.raises(gol.RunError):
+        h.wait(5)
     assert h.error and "32x32" in h.error
 
 
@@ -211,8 +215,10 @@ def test_cont_resume(gol, workdir, oracle):
     events = gol.Channel()
     h = gol.Run(p2, events, None, image_dir=str(workdir / "images"),
                 out_dir=str(workdir / "out"), resume=True)
-    assert list(events) == []
-    h.wait(5)
+    with pytest.raises(gol.RunError, match="CONT"):
+        list(events)
+    with pytest.raises(gol.RunError):
+        h.wait(5)
     assert h.error and "CONT" in h.error
 
 
@@ -240,10 +246,20 @@ def test_baseline_configs_through_run(gol, workdir, oracle, key, ngpus):
     _write_random_pgm(workdir, oracle, d["seed"], w, h)
     p = gol.Params(Turns=turns, Threads=8, ImageWidth=w, ImageHeight=h)
     kw = dict(ngpus=ngpus, devices=[0] * ngpus, halo=128) if ngpus > 1 else {}
-    evs = run_collect(gol, p, workdir, **kw)
+    # a 2 ms ticker: AliveCellsCount events at many turns of the run (the reference's 2 s
+    # ticker would fire at most once in a run this short)
+    evs = run_collect(gol, p, workdir, ticker_ms=2, **kw)
     final = [e for e in evs if isinstance(e, gol.FinalTurnComplete)]
     assert len(final) == 1 and final[0].CompletedTurns == turns
     assert len(final[0].Alive) == d["alive"]
+    # every AliveCellsCount is the oracle's count at its CompletedTurns (C2 names these
+    # events; series from tests/golden/make_alive_series.py)
+    series = G.config_alive_series(w, h, d["seed"])
+    init = oracle.popcount(oracle.gen_random(d["seed"], w, h), w)
+    ticks = [e for e in evs if isinstance(e, gol.AliveCellsCount)]
+    assert ticks, "no AliveCellsCount event"
+    for e in ticks:
+        assert e.CellsCount == (series[e.CompletedTurns] if e.CompletedTurns else init), e
     tc = [e.CompletedTurns for e in evs if isinstance(e, gol.TurnComplete)]
     assert tc == list(range(1, turns + 1))
     out = (workdir / "out" / f"{w}x{h}x{turns}.pgm").read_bytes()

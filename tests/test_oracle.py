@@ -5,6 +5,7 @@ Fixtures (tests/golden/, copied data from the reference):
   Local/images/*.pgm, digests of Local/out/*.pgm.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -153,3 +154,24 @@ def test_random_generator_definition(oracle):
             if j == nw - 1:
                 v &= (1 << 2) - 1
             assert int(w[y, j]) == v
+
+
+@pytest.mark.parametrize("key", ["5120x5120_seed1_t1000", "16384x16384_seed2_t10000"])
+def test_config_alive_series_consistent(key):
+    """The committed C2 / C3 AliveCellsCount series (make_alive_series.py) end at the
+    alive count of the committed full-size digest (make_large_digests.py): two runs of the
+    pinned bit oracle agree."""
+    import json
+    import golden_data as G
+    d = json.load(open(os.path.join(G.GOLDEN, "large_digests.json")))[key]
+    s = G.config_alive_series(d["width"], d["height"], d["seed"])
+    assert sorted(s) == list(range(1, d["turns"] + 1))
+    assert s[d["turns"]] == d["alive"]
+
+
+def test_config_alive_series_prefix(oracle):
+    """The first turns of the C2 series recomputed here with the bit oracle."""
+    import golden_data as G
+    s = G.config_alive_series(5120, 5120, 1)
+    _, counts = oracle.bit_run(oracle.gen_random(1, 5120, 5120), 5120, 20, counts=True)
+    assert [s[t] for t in range(1, 21)] == [int(c) for c in counts]
