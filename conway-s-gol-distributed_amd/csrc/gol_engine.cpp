@@ -172,7 +172,7 @@ int launch_depth(const gol_ctx *c, int64_t room)
         return 1;
     const int64_t nl = (room + c->tpl - 1) / c->tpl;
     const int k = (int)((room + nl - 1) / nl);
-    return golk::multi_ok(c->cfg.width, k) ? k : 1;
+    return golk::multi_ok(c->cfg.width, k, c->multi_variant) ? k : 1;
 }
 
 // the word layout a launch of depth k runs on
@@ -197,38 +197,57 @@ int count_now(gol_ctx *c, long long *alive)
     return GOL_OK;
 }
 
-// Create-time timing sweep of the multi-turn kernel's (turns per launch, band) on the
-// engine's own buffers.  The fastest band depends on grid/residency quantisation and on
-// whether the two boards fit the 256 MiB MALL (tools/sweep.py, tools/strip_emulate.py:
-// 65536^2 -> band 137, 8192-row strips -> 48, 16384^2 -> 20), which no closed form
-// captured, so large engines measure.  Every candidate computes the same bits.
-void autotune_multi(gol_ctx *c, bool tune_k)
+// Create-time timing sweep of the temporal-blocking kernel, its depth K and its band on
+// the engine's own buffers.  The fastest choice depends on grid/residency quantisation and
+// on whether the two boards fit the 256 MiB MALL (tools/sweep.py, tools/strip_emulate.py:
+// 65536^2 -> k_step_skew K = 8 band 137-274; 16384^2 and 8448-row strips -> k_step_wg
+// K = 12), which no closed form captured, so large engines measure.  Both kernels run on
+// the interleaved layout and every candidate computes the same bits.  `tune_variant`:
+// choose between k_step_skew and k_step_wg (otherwise keep c->multi_variant).
+void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
 {
     const long long words = (long long)c->buf_rows * c->pitch;
     if (words < (1ll << 20)) return;                 // < 64 Mi cells: keep the defaults
-    static const int kKs[] = {6, 8};   // K = 7 measured no faster (DESIGN)
-    static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
-    // plus the bands whose grid just fits 1..4 rounds of resident wavefronts (65536^2 at 4
-    // waves/SIMD: 274 -> 4080 of 4096 waves, 137 -> 8160 of 8192)
-    std::vector<int> bands(std::begin(kBands), std::end(kBands));
-    {
-        int ncu = 0;
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
-        const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
+    std::vector<int> vars{c->multi_variant};
+    if (tune_variant) vars = {golk::kMultiSkewILW16, golk::kMultiWg};
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+    struct Cand {
+        int var, K, band;
+    };
+    std::vector<Cand> cand;
+    for (int var : vars) {
+        // K = 7 measured no faster than 6 / 8 on k_step_skew (DESIGN); k_step_wg goes to 16
+        std::vector<int> ks = golk::multi_max_turns(var) > 8 ? std::vector<int>{8, 12, 16}
+                                                            : std::vector<int>{6, 8};
+        if (!tune_k) ks = {c->tpl};
+        static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
+        const int lane_dw = golk::multi_lane_dwords(c->multi_words, var);
         const long long ntx = golk::multi_tiles(c->cfg.width, lane_dw);
-        for (int K : kKs) {
-            const long long cap =
-                (long long)ncu * 4 * golk::multi_blocks_per_cu(K, c->multi_words, c->multi_variant);
+        for (int K : ks) {
+            if (!golk::multi_ok(c->cfg.width, K, var)) continue;
+            // plus the bands whose grid just fits 1..4 rounds of resident band pipelines
+            // (k_step_skew: one per wave, k_step_wg: one per workgroup; 65536^2 at 4
+            // waves/SIMD: 274 -> 4080 of 4096 waves, 137 -> 8160 of 8192)
+            std::vector<int> bands(std::begin(kBands), std::end(kBands));
+            const long long cap = (long long)ncu *
+                                  golk::multi_blocks_per_cu(K, c->multi_words, var) * 4 /
+                                  golk::multi_waves_per_band(var);
             for (int r = 1; r <= 4 && cap > 0; ++r) {
                 const long long nb = r * cap / ntx;
                 if (nb <= 0) continue;
                 const long long b = (c->cfg.rows + nb - 1) / nb;
                 if (b >= 16 && b <= 1024 && b <= c->cfg.rows) bands.push_back((int)b);
             }
+            std::sort(bands.begin(), bands.end());
+            bands.erase(std::unique(bands.begin(), bands.end()), bands.end());
+            for (int band : bands) {
+                if (band > c->cfg.rows && band != bands[0]) break;
+                cand.push_back({var, K, band});
+            }
         }
-        std::sort(bands.begin(), bands.end());
-        bands.erase(std::unique(bands.begin(), bands.end()), bands.end());
     }
+    if (cand.empty()) return;
     golk::StepArgs a{};
     a.width = c->cfg.width;
     a.nw = c->nw;
@@ -240,68 +259,56 @@ void autotune_multi(gol_ctx *c, bool tune_k)
     a.cnt_hi = 0;
     a.variant = c->variant;
     a.multi_words = c->multi_words;
-    a.multi_variant = c->multi_variant;
     if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
                                  c->buf_rows, 12345, c->stream) != hipSuccess)
         return;
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return;
     if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
-    std::vector<int> ks;
-    if (tune_k) ks.assign(std::begin(kKs), std::end(kKs));
-    else ks.push_back(c->tpl);
-    std::vector<std::pair<int, int>> cand;             // (K, band)
-    for (int K : ks) {
-        if (!golk::multi_ok(c->cfg.width, K)) continue;
-        for (int band : bands) {
-            if (band > c->cfg.rows && band != bands[0]) break;
-            cand.emplace_back(K, band);
-        }
-    }
     // time `reps` launches of one candidate on the engine's stream, per turn (0 on error)
-    auto time_one = [&](int K, int band, int reps) -> float {
-        a.band = band;
+    auto time_one = [&](const Cand &cd, int reps) -> float {
+        a.band = cd.band;
+        a.multi_variant = cd.var;
         bool ok = hipEventRecord(e0, c->stream) == hipSuccess;
         for (int rep = 0; rep < reps && ok; ++rep) {
             a.in = c->board[rep & 1];
             a.out = c->board[(rep + 1) & 1];
-            ok = golk::launch_step_multi(a, K, c->stream) == hipSuccess;
+            ok = golk::launch_step_multi(a, cd.K, c->stream) == hipSuccess;
         }
         ok = ok && hipEventRecord(e1, c->stream) == hipSuccess &&
              hipEventSynchronize(e1) == hipSuccess;
         float ms = 0.f;
         if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return 0.f;
-        return ms / ((float)reps * K);
+        return ms / ((float)reps * cd.K);
     };
     // the clock ramps over the first milliseconds of load: warm up, then two interleaved
     // passes over the candidates, best of the two per candidate (one pass picked bands
-    // 73 / 137 / 218 at 65536^2 on three runs)
-    // passes; each candidate times >= ~1 ms of launches (strips of 8192 rows launch in ~50 us)
+    // 73 / 137 / 218 at 65536^2 on three runs); each candidate times >= ~1 ms of launches
+    // (strips of 8192 rows launch in ~50 us)
     std::vector<float> t(cand.size(), 0.f);
     int reps = 3;
-    if (!cand.empty()) {
-        const int K = cand.back().first;
-        const float us = time_one(K, cand.back().second, 12) * 1000.f * K;   // per launch
+    {
+        const float us = time_one(cand.back(), 12) * 1000.f * cand.back().K;   // per launch
         if (us > 0.f) reps = std::max(3, std::min(24, (int)(1000.f / us) + 1));
     }
     for (int pass = 0; pass < 2; ++pass)
         for (size_t i = 0; i < cand.size(); ++i) {
-            const float v = time_one(cand[i].first, cand[i].second, reps);
+            const float v = time_one(cand[i], reps);
             if (v > 0.f && (t[i] == 0.f || v < t[i])) t[i] = v;
         }
     float best = 0.f;
-    int best_k = c->tpl, best_b = c->band_multi;
+    Cand pick{c->multi_variant, c->tpl, c->band_multi};
     for (size_t i = 0; i < cand.size(); ++i)
         if (t[i] > 0.f && (best == 0.f || t[i] < best)) {
             best = t[i];
-            best_k = cand[i].first;
-            best_b = cand[i].second;
+            pick = cand[i];
         }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipGetLastError();
-    c->tpl = best_k;
-    c->band_multi = best_b;
+    c->multi_variant = pick.var;
+    c->tpl = pick.K;
+    c->band_multi = pick.band;
     c->tuned_us_per_turn = best * 1000.f;
 }
 
@@ -382,9 +389,11 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     }
     const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
     const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
-    c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch : (auto_bm >= 48 ? 8 : 6);
+    const bool wg = golk::multi_max_turns(c->multi_variant) > 8;
+    c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch
+                                       : (wg ? 16 : (auto_bm >= 48 ? 8 : 6));
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
-    c->tpl = std::max(1, std::min(c->tpl, golk::kMaxTurnsPerLaunch));
+    c->tpl = std::max(1, std::min(c->tpl, golk::multi_max_turns(c->multi_variant)));
     if (c->fast && c->tpl > 1 && !golk::multi_fits(c->nw, c->pitch, c->buf_rows))
         c->blocking_limited = true;   // reported in gol_info.blocking_limited
     if (!c->fast || c->blocking_limited) c->tpl = 1;
@@ -397,7 +406,8 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         const int bpc = golk::multi_blocks_per_cu(c->tpl, c->multi_words, c->multi_variant);
         c->band_multi = golk::pick_band_multi(cfg->width, cfg->rows, lane_dw, c->tpl,
-                                              ncu * bpc * 4);
+                                              ncu * bpc * 4 /
+                                                  golk::multi_waves_per_band(c->multi_variant));
     }
     if (c->band_multi <= 0) c->band_multi = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
     const size_t words = (size_t)c->buf_rows * c->pitch;
@@ -421,7 +431,11 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     c->stream = c->own_stream;
     if (c->tpl > 1 && cfg->band_rows <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {
         const char *at = getenv("GOL_AUTOTUNE");
-        if (!at || atoi(at) != 0) autotune_multi(c, cfg->turns_per_launch <= 0);
+        // the kernel is tuned too unless an experiment pins it (GOL_MULTI_VARIANT) or the
+        // requested depth only one of them runs
+        const bool tune_var = !getenv("GOL_MULTI_VARIANT") && c->multi_words == 1 &&
+                              (cfg->turns_per_launch <= 0 || cfg->turns_per_launch <= 8);
+        if (!at || atoi(at) != 0) autotune_multi(c, cfg->turns_per_launch <= 0, tune_var);
     }
     if ((e = hipMemsetAsync(c->board[0], 0, words * 8, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->board[1], 0, words * 8, c->stream)) != hipSuccess ||
@@ -593,6 +607,46 @@ int gol_fill_random(gol_ctx *c, uint64_t seed)
 
 namespace {
 
+// Tools only (GOL_MULTI_VARIANT=kMultiWgDiag): one k_step_wg launch with per-wave wait
+// timing, summarised by wave role on stderr.
+int wg_diag_launch(gol_ctx *c, golk::StepArgs a, int k)
+{
+    const long long ntx = golk::multi_tiles(c->cfg.width, 2);
+    const long long pipes = ntx * ((a.row_hi - a.row_lo + a.band - 1) / a.band);
+    const size_t n = (size_t)pipes * 4 * 8;
+    unsigned long long *d = nullptr;
+    HIP_OR_FAIL(c, hipMalloc(&d, n * 8));
+    HIP_OR_FAIL(c, hipMemsetAsync(d, 0, n * 8, c->stream));
+    a.counts = d;
+    HIP_OR_FAIL(c, golk::launch_step_multi(a, k, c->stream));
+    std::vector<unsigned long long> h(n);
+    HIP_OR_FAIL(c, hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    (void)hipFree(d);
+    unsigned long long t0min = ~0ull, t1max = 0;
+    for (long long p = 0; p < pipes; ++p)
+        for (int w = 0; w < 4; ++w) {
+            const unsigned long long *e = &h[((size_t)p * 4 + w) * 8];
+            t0min = std::min(t0min, e[7]);
+            t1max = std::max(t1max, e[7] + e[0]);
+        }
+    for (int w = 0; w < 4; ++w) {
+        double life = 0, first = 0, fw = 0, nf = 0, ew = 0, ne = 0, nl = 0;
+        for (long long p = 0; p < pipes; ++p) {
+            const unsigned long long *e = &h[((size_t)p * 4 + w) * 8];
+            life += (double)e[0]; first += (double)e[1]; fw += (double)e[2];
+            nf += (double)e[3]; ew += (double)e[4]; ne += (double)e[5]; nl += (double)e[6];
+        }
+        fprintf(stderr,
+                "wg_diag K=%d band=%d pipes=%lld wave %d: life %.0f ticks, first-row wait %.1f%%, "
+                "fetch waits %.1f%% (%.2f per row), emit waits %.1f%% (%.2f per row)\n",
+                k, a.band, pipes, w, life / pipes, 100 * first / life, 100 * fw / life, nf / nl,
+                100 * ew / life, ne / nl);
+    }
+    fprintf(stderr, "wg_diag launch span %llu ticks\n", t1max - t0min);
+    return GOL_OK;
+}
+
 constexpr int kCtlDepth = 2;   // launches queued ahead while a control word is in use
 
 // gol_step / gol_step_overlap.  xstream != null: the first launch is split -- the rows
@@ -679,7 +733,9 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
             a.blocked = nullptr;
             a.counts = nullptr;
             a.band = c->band_multi;
-            if (split && in_lo < in_hi) {
+            if (c->multi_variant == golk::kMultiWgDiag && !split) {
+                if (int rc = wg_diag_launch(c, a, k)) return rc;
+            } else if (split && in_lo < in_hi) {
                 golk::StepArgs b = a;
                 b.row_lo = in_lo;
                 b.row_hi = in_hi;

@@ -39,7 +39,11 @@ enum : int {
     kMultiSkewD1 = 5,       // k_step_skew, 1 dword (32 cells) per lane     (V = 1, K = 4/6/8 only)
     kMultiSkewIL = 6,       // k_step_skew on the interleaved board layout (V = 1)
     kMultiSkewILW16 = 7,    // kMultiSkewIL, one 16-B row DMA from half the lanes (V = 1; default)
-    kMultiCount = 8,
+    kMultiWg = 8,           // k_step_wg: one band's stages split over the 4 waves of a workgroup
+                            //   (interleaved layout, V = 1, K = 4..16; K = 2, 3: kMultiSkewILW16)
+    kMultiWgNoBar = 10,     // k_step_wg without hand-off sync: timing ablation (wrong results)
+    kMultiWgDiag = 11,      // k_step_wg with per-wave wait timing (tools/wg_diag.py)
+    kMultiCount = 12,
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 
@@ -60,11 +64,14 @@ bool fast_path_ok(int width);
 
 // K turns per launch (temporal blocking): outputs rows [row_lo, row_hi) after `turns`
 // turns, reading rows [row_lo - turns, row_hi + turns) (mod modrows).  No blocked mask,
-// no counts.  turns in {2, 3, 4, 5, 6, 8}.
-constexpr int kMaxTurnsPerLaunch = 8;
+// no counts.  turns in 2 .. multi_max_turns(variant).
+constexpr int kMaxTurnsPerLaunch = 16;
+int multi_max_turns(int variant);       // 16 for kMultiWg, 8 for the k_step_skew variants
 // band height of the boundary launches of an overlapped step (rows next to the halos)
 constexpr int kOverlapBand = 16;
-bool multi_ok(int width, int turns);
+bool multi_ok(int width, int turns, int variant);
+// waves sharing one band pipeline (4 for kMultiWg, else 1)
+int multi_waves_per_band(int variant);
 bool multi_fits(int nw, int pitch, int rows);   // buffer < 2 GiB (k_step_skew buffer ranges)
 // the temporal-blocking kernel for (words per lane, variant) runs on the interleaved layout
 bool multi_is_il(int words_per_lane, int variant);

@@ -31,6 +31,8 @@ def main():
                     help="exchange through RCCL at world size 1 (rank 0 is its own neighbour, "
                          "zero-copy board views): direct RCCL calls on the engine stream, or "
                          "torch batch_isend_irecv; default: local copies")
+    ap.add_argument("--overlap", action="store_true",
+                    help="--rccl direct: overlapped exchange (gol_step_overlap)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ds_for = None
@@ -44,7 +46,7 @@ def main():
         if a.rccl == "direct":
             from gol.rccl import RcclComm
             comm = RcclComm(0, 1, dev)
-        ds_for = lambda es: DistStrip(es, 0, 1, rccl=comm)  # noqa: E731
+        ds_for = lambda es: DistStrip(es, 0, 1, rccl=comm, overlap=a.overlap)  # noqa: E731
     if a.full:
         e = gol.Engine(a.size, a.size, device=0)
         e.fill_random(3)
