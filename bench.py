@@ -73,9 +73,12 @@ def parse():
                          "0 = skip)")
     ap.add_argument("--c3-turns", type=int, default=10000,
                     help="turns of the second config (configs[2]: 10000)")
-    ap.add_argument("--overlap", type=int, default=1,
-                    help="N > 1, direct RCCL: overlap the halo exchange with the first "
-                         "launch's interior rows (gol_step_overlap); 0 = serialised")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="N > 1, direct RCCL: 1 = overlap the halo exchange with the first "
+                         "launch's interior rows (gol_step_overlap, RCCL on its own stream); "
+                         "0 (default) = exchange on the engine stream, serialised: measured "
+                         "faster at halo 128 (8-strip shape, one GPU exchanging with itself: "
+                         "6.12 vs 6.52 us/turn, profiles/r02_overlap_strip8.log)")
     ap.add_argument("--transport", choices=("rccl", "torch"), default="rccl",
                     help="N > 1 halo transport on the nccl backend: direct RCCL send/recv on "
                          "the engine's stream (default) or torch batch_isend_irecv")

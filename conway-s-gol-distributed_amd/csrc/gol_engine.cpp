@@ -218,8 +218,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     std::vector<Cand> cand;
     for (int var : vars) {
         // K = 7 measured no faster than 6 / 8 on k_step_skew (DESIGN); k_step_wg goes to 16
-        std::vector<int> ks = golk::multi_max_turns(var) > 8 ? std::vector<int>{8, 12, 16}
-                                                            : std::vector<int>{6, 8};
+        std::vector<int> ks = golk::multi_waves_per_band(var) > 1 ? std::vector<int>{8, 12, 16}
+                                                            : std::vector<int>{6, 8, 10};
         if (!tune_k) ks = {c->tpl};
         static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
         const int lane_dw = golk::multi_lane_dwords(c->multi_words, var);
@@ -297,12 +297,21 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             if (v > 0.f && (t[i] == 0.f || v < t[i])) t[i] = v;
         }
     float best = 0.f;
-    Cand pick{c->multi_variant, c->tpl, c->band_multi};
     for (size_t i = 0; i < cand.size(); ++i)
-        if (t[i] > 0.f && (best == 0.f || t[i] < best)) {
-            best = t[i];
+        if (t[i] > 0.f && (best == 0.f || t[i] < best)) best = t[i];
+    // within 1.5 % of the best, the deepest K wins: the same steady rate with fewer launches
+    // when a run is short (65536^2, 20 turns: K = 10 -> 2 launches, 104.7k GCUPS; K = 8 ->
+    // 7 + 7 + 6, 100.8k; steady state 36.0 vs 36.2 us/turn)
+    Cand pick{c->multi_variant, c->tpl, c->band_multi};
+    float pick_t = 0.f;
+    for (size_t i = 0; i < cand.size(); ++i) {
+        if (t[i] <= 0.f || t[i] > best * 1.015f) continue;
+        if (pick_t == 0.f || cand[i].K > pick.K || (cand[i].K == pick.K && t[i] < pick_t)) {
             pick = cand[i];
+            pick_t = t[i];
         }
+    }
+    if (pick_t > 0.f) best = pick_t;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipGetLastError();
@@ -389,7 +398,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     }
     const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
     const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
-    const bool wg = golk::multi_max_turns(c->multi_variant) > 8;
+    const bool wg = golk::multi_waves_per_band(c->multi_variant) > 1;
     c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch
                                        : (wg ? 16 : (auto_bm >= 48 ? 8 : 6));
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);

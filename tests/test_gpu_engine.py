@@ -228,7 +228,7 @@ def test_il_layout_roundtrip():
 
 
 @pytest.mark.parametrize("mv", [6, 7])
-@pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 19), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (2048, 300, 137, 17),
                                             (8064, 33, 16, 8), (7936, 20, 9, 16)])

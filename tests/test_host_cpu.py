@@ -76,11 +76,11 @@ def test_run_requires_native_library(monkeypatch, tmp_path):
 
 
 def _kernel_rule(name):
-    """The body of a device rule function in gol_kernels.hip as (dst, op, args) triples."""
+    """The body of a device rule function in gol_device.h as (dst, op, args) triples."""
     import os
     import re
     src = open(os.path.join(os.path.dirname(__file__), "..", "conway-s-gol-distributed_amd",
-                            "csrc", "gol_kernels.hip")).read()
+                            "csrc", "gol_device.h")).read()
     body = src[src.index(f"uint32_t {name}("):]
     body = body[body.index("{") + 1:body.index("\n}")]
     ops = []
