@@ -1,14 +1,26 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile.sh run (gpurun_out/prof) into profiles/<tag>_*.{csv,json}.
+"""Summarise a rocprofv3 run of bench.py into profiles/<tag>_*.{csv,json}.
 
-traffic per launch = (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 bytes for the stencil kernel,
-medians over the last 20 dispatches of the top kernel (the timed launches):
+Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD]
+  SRC    the pass directory root (tools/profile_r02.sh: gpurun_out/prof2)
+  KT     the --kernel-trace --stats pass (KT/ + KT.log holding the bench line), or - for
+         a PMC-only summary
+  FETCH / WRITE  the --pmc FETCH_SIZE / WRITE_SIZE passes of the same workload
+  BOARD  which board of the bench run: 0 = the headline board, 1 = configs_measured[0]
+
+Timed dispatches: bench.py loads each board (k_il_convert), steps the warm-up turns, then
+the timed turns, so the timed launches are the last `launches` stencil dispatches
+(k_step*) before the next board's k_fill_random (the engine's create-time autotune also
+dispatches the stencil, on other bands, so "the last N of the top kernel" is not enough).
+Their names can mix K: the engine spreads T turns evenly over ceil(T / K) launches.
+
+traffic per launch = (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 bytes, medians over the last 20
+stencil dispatches of the PMC pass's first board (a run with --c3-size 0, one board):
 FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads exactly half of a wide
 (16 B/lane) coalesced stream (MI355X_MICROARCH.md, HBM section) and of the stencil's own
 4-B/lane LDS-DMA row stream (tools/calib/calib_fetch.hip: 0.501 GiB for 1 GiB), so it is
-doubled;
-WRITE_SIZE is exact for 16-B-per-lane stores.  Infinity-Cache hits are included in
-both, so this is fabric traffic out of the XCD L2s (an upper bound on HBM bytes)."""
+doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  Infinity-Cache hits are included
+in both, so this is fabric traffic out of the XCD L2s (an upper bound on HBM bytes)."""
 import csv
 import json
 import os
@@ -19,48 +31,68 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(tag, src=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_step"):
+def board_segments(rows):
+    """Split time-ordered dispatch rows into per-board stepping segments: the dispatches
+    after each k_il_convert (board load) up to the next k_fill_random (next engine)."""
+    segs, cur = [], None
+    for r in rows:
+        name = r["Kernel_Name"]
+        if "k_il_convert" in name:
+            cur = []
+            segs.append(cur)
+        elif "k_fill_random" in name:
+            cur = None
+        elif cur is not None and "k_step" in name:
+            cur.append(r)
+    return segs
+
+
+def load_rows(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return rows
+
+
+def main(tag, src, kt, fetch=None, write=None, board="0"):
+    board = int(board)
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
-    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"),
-                os.path.join(out, f"{tag}_kernel_stats.csv"))
-    stats = list(csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))))
-    top = max(stats, key=lambda r: float(r["TotalDurationNs"]))
-    res = {"kernel": top["Name"], "calls": int(top["Calls"]),
-           "avg_ns": float(top["AverageNs"]), "min_ns": float(top["MinNs"]),
-           "max_ns": float(top["MaxNs"]), "share_pct": float(top["Percentage"])}
-    # the bench's timed region = its last `launches` dispatches of the top kernel: average
-    # exactly those (the trace also holds autotune / warm-up dispatches of the same kernel)
-    import re
-    log = os.path.join(src, "kt.log")
-    trace = os.path.join(src, "kt", "run_kernel_trace.csv")
-    if os.path.exists(log) and os.path.exists(trace):
-        m = re.search(r'"launches": (\d+)', open(log).read())
-        if m:
-            n = int(m.group(1))
-            disp = [r for r in csv.DictReader(open(trace)) if r["Kernel_Name"] == top["Name"]]
-            disp.sort(key=lambda r: int(r["Start_Timestamp"]))
-            last = disp[-n:]
-            durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in last]
-            res["timed_launches"] = len(last)
-            res["timed_avg_ns"] = statistics.mean(durs)
-            res["timed_span_avg_ns"] = (int(last[-1]["End_Timestamp"]) -
-                                        int(last[0]["Start_Timestamp"])) / len(last)
-            for ln in open(log).read().splitlines():
-                if ln.startswith('{"metric"'):
-                    res["bench_line"] = json.loads(ln)
-    for name, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-        p = os.path.join(src, name, "run_counter_collection.csv")
-        if not os.path.exists(p):
+    res = {"source": f"{os.path.relpath(src, ROOT)}/{kt}", "board": board}
+    line = None
+    if kt != "-":
+        shutil.copy(os.path.join(src, kt, "run_kernel_stats.csv"),
+                    os.path.join(out, f"{tag}_kernel_stats.csv"))
+        for ln in open(os.path.join(src, kt + ".log")).read().splitlines():
+            if ln.startswith('{"metric"'):
+                line = json.loads(ln)
+    if line is not None:
+        res["bench_line"] = line
+        if board == 0:
+            n, bench_us = line["roofline"]["launches"], line["roofline"]["launch_us"]
+        else:
+            c = line["configs_measured"][board - 1]
+            n, bench_us = c["launches"], c["launch_us"]
+        segs = board_segments(load_rows(os.path.join(src, kt, "run_kernel_trace.csv")))
+        last = segs[board][-n:]
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last]
+        names = {}
+        for r in last:
+            names[r["Kernel_Name"]] = names.get(r["Kernel_Name"], 0) + 1
+        res.update({
+            "timed_launches": len(last), "timed_kernels": names,
+            "timed_avg_ns": statistics.mean(durs),
+            "timed_span_avg_ns": (int(last[-1]["End_Timestamp"]) -
+                                  int(last[0]["Start_Timestamp"])) / len(last),
+            "bench_hip_event_launch_us": bench_us})
+    for name, counter in ((fetch, "FETCH_SIZE"), (write, "WRITE_SIZE")):
+        if not name or name == "-":
             continue
-        # the bench's timed launches are the last dispatches of the top kernel; the
-        # engine's create-time autotune dispatches the same kernel on other bands first
-        rows = [r for r in csv.DictReader(open(p))
-                if r["Kernel_Name"] == top["Name"] and r["Counter_Name"] == counter]
-        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        rows = rows[-20:]
-        res[counter + "_kib_median"] = statistics.median(float(r["Counter_Value"]) for r in rows)
-        res[counter + "_launches"] = len(rows)
+        rows = [r for r in load_rows(os.path.join(src, name, "run_counter_collection.csv"))
+                if r["Counter_Name"] == counter]
+        seg = board_segments(rows)[0][-20:]
+        res[counter + "_kernels"] = sorted({r["Kernel_Name"] for r in seg})
+        res[counter + "_kib_median"] = statistics.median(float(r["Counter_Value"]) for r in seg)
+        res[counter + "_launches"] = len(seg)
     if "FETCH_SIZE_kib_median" in res and "WRITE_SIZE_kib_median" in res:
         rd = res["FETCH_SIZE_kib_median"] * 2 * 1024
         wr = res["WRITE_SIZE_kib_median"] * 1024
@@ -69,7 +101,8 @@ def main(tag, src=os.path.join(ROOT, "gpurun_out", "prof"), kernel="k_step"):
         res["traffic_bytes_per_launch"] = rd + wr
     with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps(res, indent=1))
+    show = {k: v for k, v in res.items() if k != "bench_line"}
+    print(json.dumps(show, indent=1))
 
 
 if __name__ == "__main__":
