@@ -209,7 +209,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     const long long words = (long long)c->buf_rows * c->pitch;
     if (words < (1ll << 20)) return;                 // < 64 Mi cells: keep the defaults
     std::vector<int> vars{c->multi_variant};
-    if (tune_variant) vars = {golk::kMultiSkewILW16, golk::kMultiWg};
+    if (tune_variant) vars = {golk::kMultiSkewILW16, golk::kMultiWg, golk::kMultiWgHx};
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     struct Cand {
@@ -223,7 +223,6 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
         if (!tune_k) ks = {c->tpl};
         static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
         const int lane_dw = golk::multi_lane_dwords(c->multi_words, var);
-        const long long ntx = golk::multi_tiles(c->cfg.width, lane_dw);
         for (int K : ks) {
             if (!golk::multi_ok(c->cfg.width, K, var)) continue;
             // plus the bands whose grid just fits 1..4 rounds of resident band pipelines
@@ -231,13 +230,15 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             // waves/SIMD: 274 -> 4080 of 4096 waves, 137 -> 8160 of 8192)
             std::vector<int> bands(std::begin(kBands), std::end(kBands));
             const long long cap = (long long)ncu *
-                                  golk::multi_blocks_per_cu(K, c->multi_words, var) * 4 /
-                                  golk::multi_waves_per_band(var);
+                                  golk::multi_blocks_per_cu(K, c->multi_words, var) *
+                                  golk::multi_pipes_per_block(var);
             for (int r = 1; r <= 4 && cap > 0; ++r) {
-                const long long nb = r * cap / ntx;
-                if (nb <= 0) continue;
-                const long long b = (c->cfg.rows + nb - 1) / nb;
-                if (b >= 16 && b <= 1024 && b <= c->cfg.rows) bands.push_back((int)b);
+                // the smallest band whose launch fits r rounds
+                for (int b = 16; b <= 1024 && b <= c->cfg.rows; ++b)
+                    if (golk::multi_pipes(c->cfg.width, c->cfg.rows, b, lane_dw, var) <= r * cap) {
+                        bands.push_back(b);
+                        break;
+                    }
             }
             std::sort(bands.begin(), bands.end());
             bands.erase(std::unique(bands.begin(), bands.end()), bands.end());
@@ -415,8 +416,9 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         const int bpc = golk::multi_blocks_per_cu(c->tpl, c->multi_words, c->multi_variant);
         c->band_multi = golk::pick_band_multi(cfg->width, cfg->rows, lane_dw, c->tpl,
-                                              ncu * bpc * 4 /
-                                                  golk::multi_waves_per_band(c->multi_variant));
+                                              ncu * bpc *
+                                                  golk::multi_pipes_per_block(c->multi_variant),
+                                              c->multi_variant);
     }
     if (c->band_multi <= 0) c->band_multi = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
     const size_t words = (size_t)c->buf_rows * c->pitch;

@@ -41,6 +41,8 @@ enum : int {
     kMultiSkewILW16 = 7,    // kMultiSkewIL, one 16-B row DMA from half the lanes (V = 1; default)
     kMultiWg = 8,           // k_step_wg: one band's stages split over the 4 waves of a workgroup
                             //   (interleaved layout, V = 1, K = 4..16; K = 2, 3: kMultiSkewILW16)
+    kMultiWgHx = 9,         // k_step_wg on helix tiles: the row bands end to end, cut every 62
+                            //   lanes (no per-row remainder tile; needs nw even)
     kMultiWgNoBar = 10,     // k_step_wg without hand-off sync: timing ablation (wrong results)
     kMultiWgDiag = 11,      // k_step_wg with per-wave wait timing (tools/wg_diag.py)
     kMultiCount = 12,
@@ -72,6 +74,8 @@ constexpr int kOverlapBand = 16;
 bool multi_ok(int width, int turns, int variant);
 // waves sharing one band pipeline (4 for kMultiWg, else 1)
 int multi_waves_per_band(int variant);
+// band pipelines per thread block (k_step_skew: 4 single-wave pipelines; k_step_wg: 1)
+int multi_pipes_per_block(int variant);
 bool multi_fits(int nw, int pitch, int rows);   // buffer < 2 GiB (k_step_skew buffer ranges)
 // the temporal-blocking kernel for (words per lane, variant) runs on the interleaved layout
 bool multi_is_il(int words_per_lane, int variant);
@@ -82,11 +86,15 @@ hipError_t launch_il_convert(const uint64_t *in, int in_pitch, uint64_t *out, in
 int multi_lane_dwords(int words_per_lane, int variant);
 // wavefront tiles per row band of the temporal-blocking kernel
 long long multi_tiles(int width, int lane_dwords);
+// band pipelines of one launch over `rows` rows in bands of `band` (workgroups for the
+// k_step_wg variants, wavefronts for k_step_skew): tiles x bands, or the helix tile count
+long long multi_pipes(int width, int rows, int band, int lane_dwords, int variant);
 int auto_band_multi(int width, int rows, int lane_dwords);
 // resident 256-thread blocks per CU of the temporal-blocking kernel (0 on error)
 int multi_blocks_per_cu(int turns, int words_per_lane, int variant);
 // band height minimising (residency rounds x per-wavefront work) for the multi kernel
-int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacity_waves);
+int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacity_waves,
+                    int variant);
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);

@@ -623,6 +623,8 @@ int multi_max_turns(int variant)
 
 int multi_waves_per_band(int variant) { return is_wg_variant(variant) ? 4 : 1; }
 
+int multi_pipes_per_block(int variant) { return is_wg_variant(variant) ? 1 : 4; }
+
 bool multi_is_il(int words_per_lane, int variant)
 {
     return (is_il_variant(variant) || variant >= kMultiAblate) && words_per_lane == 1;
@@ -637,6 +639,17 @@ long long multi_tiles(int width, int lane_dwords)
 {
     const long long nd = 2ll * ((width + 63) / 64);
     return (nd + 62 * lane_dwords - 1) / (62 * lane_dwords);
+}
+
+long long multi_pipes(int width, int rows, int band, int lane_dwords, int variant)
+{
+    const long long nb = (rows + band - 1) / band;
+    if (variant == kMultiWgHx) {
+        // stored virtual lanes run up to nb (nw + 4) - 3; tile t stores [62t + 1, 62t + 62]
+        const long long nwv = (width + 63) / 64 + 4;
+        return (nb * nwv - 3 + 61) / 62;
+    }
+    return multi_tiles(width, lane_dwords) * nb;
 }
 
 int auto_band_multi(int width, int rows, int lane_dwords)
@@ -664,9 +677,11 @@ bool multi_fits(int nw, int pitch, int rows)
 // k_step_skew (same interleaved layout and tiles)
 static hipError_t launch_wg(const StepArgs &a, int turns, hipStream_t s)
 {
-    const int ntx = (int)multi_tiles(a.width, 2);
-    const int nbands = (a.row_hi - a.row_lo + a.band - 1) / a.band;
-    const long long blocks = (long long)ntx * nbands;
+    const bool hx = a.multi_variant == kMultiWgHx;
+    const long long blocks =
+        multi_pipes(a.width, a.row_hi - a.row_lo, a.band, 2, a.multi_variant);
+    // band tiling: tiles per band; helix: the tile count itself (blockIdx.x = tile)
+    const int ntx = hx ? (int)blocks : (int)multi_tiles(a.width, 2);
     void *fn = wg_kernel(turns, a.multi_variant);
     if (!fn) return hipErrorInvalidValue;
     const int threads = 64 * multi_waves_per_band(a.multi_variant);
@@ -723,7 +738,8 @@ int multi_blocks_per_cu(int turns, int words_per_lane, int variant)
                                : multi_blocks_per_cu_v<2>(turns, variant);
 }
 
-int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacity_waves)
+int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacity_waves,
+                    int variant)
 {
     // Every wavefront of a launch does the same work, so a launch takes ~ rounds x
     // (per-wavefront time), rounds = ceil(waves / resident capacity): a grid that spills
@@ -733,13 +749,12 @@ int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacit
     // minimises rounds x per-wave time, charging at least 2 rounds (a single round that
     // starts and ends every wavefront together measured slower: 65536^2 K=6 band 274 vs
     // 137, 60.6 vs 58.0 us/turn); ties go to the smaller band.
-    const long long ntx = multi_tiles(width, lane_dwords);
     if (capacity_waves <= 0) return auto_band_multi(width, rows, lane_dwords);
     long long best_cost = -1;
     int best = 16;
     for (int band = 16; band <= 1024; ++band) {
         const long long nb = (rows + band - 1) / band;
-        const long long waves = ntx * nb;
+        const long long waves = multi_pipes(width, rows, band, lane_dwords, variant);
         long long rounds = (waves + capacity_waves - 1) / capacity_waves;
         if (rounds < 2) rounds = 2;
         const long long cost = rounds * ((long long)turns * band + (long long)turns * (turns + 1));

@@ -1,370 +1,7 @@
-// gol_wg.hip -- K1w k_step_wg: one band's K-stage pipeline split over the 4 wavefronts of
-// a workgroup, and its instantiation table.  Split from gol_kernels.hip so the kernel
-// families compile in parallel.
-#include "gol_device.h"
+// gol_wg.hip -- the k_step_wg instantiation table (band tiling; gol_wg_hx.hip: helix)
+#include "gol_wg.h"
 
 namespace golk {
-
-// -------------------- K1w: K turns per launch, one band's stage pipeline split over a workgroup
-// k_step_skew gives every wavefront a whole K-stage pipeline over its own band, so the
-// machine is filled with many short bands, each paying the 2K halo rows and the pipeline
-// fill again (the K^2 + K stage-rows per band), and each wave holds K x 12 VGPRs of stage
-// state (4 waves/SIMD at K = 8).  Here the NW wavefronts of a workgroup share ONE band:
-// wave w runs stages [J_w, J_w + G_w) of the same skewed pipeline (G_w = K/NW, the first
-// K%NW waves one more) and hands its last stage's rows to wave w+1 through an LDS ring.
-// For the same number of resident waves the bands are NW times taller, and a wave holds
-// ~G_w x 12 VGPRs: more waves per SIMD, or K = 16 (half the HBM bytes per turn of K = 8).
-//   * Hand-off.  Each wave boundary is a single-producer / single-consumer ring of kWgR
-//     row slots in LDS with two counters: `produced` (rows written) and `consumed` (rows
-//     read).  The producer waits for a free slot, writes the row, releases (lgkmcnt(0))
-//     and bumps `produced`; the consumer waits for `produced`, reads the row and bumps
-//     `consumed`.  Both remember the last value they saw, so in steady state most steps
-//     read no counter at all, and waves drift up to kWgR rows apart without waiting.
-//     A per-step s_barrier (lockstep) measured 22-37 % slower than no synchronisation at
-//     all; the ring keeps only the true dependencies.  The graph is a chain (wave 0 never
-//     waits upstream, the last wave never downstream), so it cannot deadlock.
-//   * Timeline.  Wave w's local pipeline is k_step_skew's with G_w stages over the
-//     nr - 2 J_w rows its first stage receives: prologue 3G-3 steps, steady loop (unroll
-//     U, a guarded tail), epilogue G-1 steps.  Its first stage consumes input row q at
-//     local step q; its last stage emits row q at local step q + 3G - 1.
-//   * Memory.  Wave 0 alone streams input rows (16-B LDS-DMA from lanes 0..31 into its
-//     RQ-slot ring, counted vmcnt wait: it issues no stores, so the count is exact); the
-//     last wave alone stores output rows.  Tiles, halo lanes, interleaved layout, rule and
-//     buffer addressing are k_step_skew's (IL, W16, BUF, R7).
-template <int K, int NW>
-struct WgSplit {
-    static constexpr int G(int w) { return K / NW + (w < K % NW ? 1 : 0); }
-    static constexpr int J(int w) { return w == 0 ? 0 : J(w - 1) + G(w - 1); }
-};
-
-// Ring slots are compile-time (immediate LDS offsets): the steady loop is unrolled by
-// U = lcm(3, kWgRQ, kWgR) = 6.  Runtime slot indices (to deepen the rings to 12 DMA rows
-// and 8 hand-off slots without a longer unroll) measured no faster and cost ~10 VGPRs
-// (K = 16: 86, i.e. 5 waves/SIMD instead of 6).
-constexpr int kWgPD = 5;                                // wave 0's rows in flight
-constexpr int kWgRQ = kWgPD + 1;                        // its LDS-DMA ring slots
-constexpr int kWgR = 6;                                 // hand-off ring slots per boundary
-// A wait gives up after this many polls (~2^22 x 64 cycles, >0.1 s): a broken hand-off then
-// ends the launch with a wrong board (caught by the parity tests) instead of hanging the GPU.
-constexpr int kWgSpinLimit = 1 << 22;
-constexpr int kWgLag = 3;                               // SYNC 2: consumer's initial lag (rows)
-
-struct WgShared {
-    uint32_t dma[kWgRQ][128];                           // wave 0's input rows (64 words each)
-    uint32_t xfer[3][kWgR][128];                        // wave w -> w+1 rows (NW <= 4)
-    uint32_t produced[4], consumed[4];                  // per boundary: rows written / read
-};
-
-__device__ __forceinline__ uint32_t lds_load_counter(const uint32_t *p)
-{
-    return (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-}
-__device__ __forceinline__ void lds_store_counter(uint32_t *p, uint32_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// SYNC: 0 = timing ablation only (no hand-off synchronisation: wrong results); 1 = counters
-// with hardware release/acquire (s_waitcnt lgkmcnt(0) around every hand-off); 2 = counters
-// ordered by the LDS itself (it executes a CU's requests in arrival order, and each wave's
-// in issue order: a row written before its counter is visible to a reader that saw the
-// counter; a slot read before its `consumed` store is read before the producer can see
-// that store and overwrite it) with compiler-only fences, and a consumer that starts
-// kWgLag rows behind its producer so the ring absorbs rate jitter both ways.  3 = 2 plus
-// per-wave wait timing into a.counts (tools only: GOL_MULTI_VARIANT=kMultiWgDiag).
-template <int K, int NW, int W, int SYNC>
-__device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
-                                        const StepArgs &a, WgShared &sh, int tx, int y0, int y1,
-                                        int nr)
-{
-    constexpr int ND = 2;
-    constexpr int G = WgSplit<K, NW>::G(W);
-    constexpr int J = WgSplit<K, NW>::J(W);
-    constexpr bool FIRST = W == 0, LAST = W == NW - 1;
-    constexpr int RQ = kWgRQ, PD = kWgPD, R = kWgR;
-    constexpr int U = 6;                                 // lcm(3, RQ, R): slots are immediates
-    static_assert(U % 3 == 0 && U % RQ == 0 && U % R == 0, "steady unroll");
-    constexpr int S0_ = 3 * G - 3;                       // local prologue steps
-    constexpr int EMIT0 = 3 * G - 1;                     // first local step the last stage emits
-    constexpr int STRIDE = 62 * ND, SHIFT = ND;
-    static_assert(NW >= 2 && NW <= 4 && G >= 1, "2..4 waves, every wave a stage");
-    const int lane = threadIdx.x & 63;
-    const int nl = nr - 2 * J;                           // rows this wave's first stage takes
-
-    const int nd = 2 * a.nw;
-    const int t0 = tx * STRIDE + SHIFT;
-    const int t1 = min(t0 + STRIDE, nd + SHIFT);
-    const int last = (t1 - t0 + ND - 1) / ND + 1;        // right halo lane
-    const bool st = lane >= 1 && lane < last;
-    int w = t0 - ND + ND * lane;                         // lane's first dword (torus wrap)
-    while (w >= nd) w -= nd;
-    const uint32_t lane_b = (uint32_t)w * 4u;
-    int pw = t0 - ND + 4 * (lane & 31);                  // W16 DMA: words 2L, 2L+1
-    while (pw >= nd) pw -= nd;
-    const uint32_t lane_dma = (uint32_t)pw * 4u;
-    const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
-    const int M = a.modrows;
-    const uint32_t span = (uint32_t)M * pitch_b;
-    auto rowoff = [&](int r) -> uint32_t {
-        while (r < 0) r += M;
-        while (r >= M) r -= M;
-        return (uint32_t)r * pitch_b;
-    };
-    auto adv = [&](uint32_t &o) {
-        o += pitch_b;
-        o = o >= span ? o - span : o;
-    };
-    const __amdgpu_buffer_rsrc_t rin =
-        __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)span, kBufFlags);
-    const __amdgpu_buffer_rsrc_t rout =
-        __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)span, kBufFlags);
-
-    uint32_t ld_off = 0;
-    auto issue = [&](auto Qc) {                          // wave 0: next input row -> slot Q
-        constexpr int q = decltype(Qc)::value;
-        if (lane < 32)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (lds_void *)&sh.dma[q][0], 16,
-                                                     lane_dma, ld_off, 0, 0);
-        adv(ld_off);
-    };
-    // priorities graded down the chain: upstream waves outrank their consumers (equal
-    // priorities left the followers waiting for the head's rows at ~93 % of their steps,
-    // tools/wg_diag.py; graded: 65536^2 K=16 44.6 -> 38.2 us/turn)
-    if constexpr (SYNC >= 2) __builtin_amdgcn_s_setprio(NW - 1 - W);
-    uint32_t avail = 0;                                  // consumer: rows known to be written
-    uint32_t room = R;                                   // producer: rows it may write
-    constexpr bool DIAG = SYNC == 3;
-    unsigned long long d_t0 = DIAG ? __builtin_amdgcn_s_memtime() : 0, d_fw = 0, d_ew = 0,
-                       d_nf = 0, d_ne = 0, d_first = 0;
-    // input row q of local step l == q (SM = l mod U): wave 0 from its DMA ring, the others
-    // from the upstream hand-off ring
-    auto lds_order = [] { __atomic_signal_fence(__ATOMIC_SEQ_CST); };   // compiler-only
-    auto fetch = [&](auto SMc, int q, uint32_t (&c)[ND]) {
-        constexpr int SM = decltype(SMc)::value;
-        if constexpr (FIRST) {
-            __builtin_amdgcn_s_waitcnt(((PD - 1) & 15) | (((PD - 1) >> 4) << 14) | (7 << 4) |
-                                       (15 << 8));
-            const uint32_t *sp = &sh.dma[SM % RQ][2 * lane];
-            c[0] = sp[0];
-            c[1] = sp[1];
-        } else {
-            if constexpr (SYNC != 0) {
-                uint32_t need = (uint32_t)q + 1;
-                if constexpr (SYNC >= 2)
-                    if (q == 0) need = (uint32_t)min(kWgLag + 1, nl);   // start behind
-                unsigned long long tw = 0;
-                if (DIAG && avail < need) tw = __builtin_amdgcn_s_memtime();
-                for (int spin = 0; avail < need && spin < kWgSpinLimit; ++spin) {
-                    avail = lds_load_counter(&sh.produced[W - 1]);
-                    if (avail < need) __builtin_amdgcn_s_sleep(1);
-                }
-                if (DIAG && tw) {
-                    const unsigned long long dt = __builtin_amdgcn_s_memtime() - tw;
-                    if (q == 0) d_first += dt;
-                    else { d_fw += dt; ++d_nf; }
-                }
-                if constexpr (SYNC == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-                else lds_order();
-            }
-            const uint32_t *sp = &sh.xfer[W - 1][SM % R][2 * lane];
-            c[0] = sp[0];
-            c[1] = sp[1];
-            if constexpr (SYNC != 0) {
-                // the row is read before the slot is handed back
-                if constexpr (SYNC == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-                else lds_order();
-                if (lane == 0) lds_store_counter(&sh.consumed[W - 1], (uint32_t)q + 1);
-            }
-        }
-    };
-    auto emit = [&](auto SMc, int q, const uint32_t (&o)[ND]) {   // non-last waves: row q
-        constexpr int SM = decltype(SMc)::value;
-        constexpr int slot = ((SM - EMIT0) % R + R) % R;
-        if constexpr (SYNC != 0) {
-            unsigned long long tw = 0;
-            if (DIAG && room <= (uint32_t)q) tw = __builtin_amdgcn_s_memtime();
-            for (int spin = 0; room <= (uint32_t)q && spin < kWgSpinLimit; ++spin) {
-                room = lds_load_counter(&sh.consumed[W]) + R;
-                if (room <= (uint32_t)q) __builtin_amdgcn_s_sleep(1);
-            }
-            if (DIAG && tw) {
-                d_ew += __builtin_amdgcn_s_memtime() - tw;
-                ++d_ne;
-            }
-            if constexpr (SYNC == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-            else lds_order();
-        }
-        uint32_t *dp = &sh.xfer[W][slot][2 * lane];
-        dp[0] = o[0];
-        dp[1] = o[1];
-        if constexpr (SYNC != 0) {
-            if constexpr (SYNC == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            else lds_order();
-            if (lane == 0) lds_store_counter(&sh.produced[W], (uint32_t)q + 1);
-        }
-    };
-
-    uint32_t S0[G][3][ND], S1[G][3][ND], X[G][3][ND], XS[G][ND];
-#pragma unroll
-    for (int j = 0; j < G; ++j)
-#pragma unroll
-        for (int k = 0; k < ND; ++k) {
-            XS[j][k] = 0;
-#pragma unroll
-            for (int p = 0; p < 3; ++p) S0[j][p][k] = S1[j][p][k] = X[j][p][k] = 0;
-        }
-    uint32_t st_off = 0;
-    int ry = 0;                                          // last wave: row its last stage outputs
-
-    auto stage = [&](auto Jc, auto Pc, auto RULEc, const uint32_t (&x)[ND], uint32_t (&o)[ND]) {
-        constexpr int j = decltype(Jc)::value;
-        constexpr int P = decltype(Pc)::value;
-        constexpr int pm = (P + 2) % 3, po = (P + 1) % 3;
-        const uint32_t L = dpp_from_lower_z(x[ND - 1]);
-        const uint32_t Rt = dpp_from_upper_z(x[0]);
-        const uint32_t wl0 = __builtin_amdgcn_alignbit(x[1], L, 31);
-        const uint32_t er1 = __builtin_amdgcn_alignbit(Rt, x[0], 1);
-        S0[j][P][0] = xor3(wl0, x[0], x[1]);
-        S1[j][P][0] = maj(wl0, x[0], x[1]);
-        S0[j][P][1] = xor3(x[0], x[1], er1);
-        S1[j][P][1] = maj(x[0], x[1], er1);
-        X[j][P][0] = x[0];
-        X[j][P][1] = x[1];
-        if constexpr (decltype(RULEc)::value) {
-#pragma unroll
-            for (int k = 0; k < ND; ++k)
-                o[k] = life_rule7(S0[j][po][k], S0[j][pm][k], S0[j][P][k], S1[j][po][k],
-                                  S1[j][pm][k], S1[j][P][k], X[j][pm][k]);
-        }
-    };
-
-    // local step l (SM = l mod U): local stages [JA, JB) active, stages < JR apply the rule
-    auto step = [&](auto SMc, auto JAc, auto JBc, auto JRc, auto LDc, int l) {
-        constexpr int SM = decltype(SMc)::value;
-        constexpr int P = SM % 3;
-        constexpr int JA = decltype(JAc)::value, JB = decltype(JBc)::value;
-        constexpr int JR = decltype(JRc)::value;
-        using Pc = std::integral_constant<int, P>;
-        unroll_seq(std::make_integer_sequence<int, JB - JA>{}, [&](auto I) {
-            constexpr int j = JB - 1 - decltype(I)::value;
-            using RULE = std::integral_constant<bool, (j < JR)>;
-            uint32_t x[ND];
-            if constexpr (j == 0) {
-                fetch(SMc, l, x);
-            } else {
-#pragma unroll
-                for (int k = 0; k < ND; ++k) x[k] = XS[j][k];
-            }
-            if constexpr (j == G - 1) {
-                uint32_t o[ND];
-                stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, o);
-                if constexpr (RULE::value) {
-                    if constexpr (LAST) {
-                        if (st && ry >= y0 && ry < y1) buf_store(o, rout, lane_b, st_off);
-                    } else if (l >= EMIT0) {
-                        // (the last stage's first two rule steps, S0_ and S0_ + 1, still
-                        // fill its window: k_step_skew drops those rows by the row check)
-                        emit(SMc, l - EMIT0, o);
-                    }
-                }
-            } else {
-                stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, XS[j + 1]);
-            }
-        });
-        if constexpr (FIRST && decltype(LDc)::value) issue(std::integral_constant<int, (SM + PD) % RQ>{});
-        if constexpr (LAST && JR == G) {
-            adv(st_off);
-            ++ry;
-        }
-    };
-    using Tt = std::true_type;
-    using Ft = std::false_type;
-    using Z = std::integral_constant<int, 0>;
-    using Gc = std::integral_constant<int, G>;
-
-    if constexpr (FIRST) {
-        ld_off = rowoff(y0 - K);                         // input row r_first = y0 - K
-        unroll_seq(std::make_integer_sequence<int, PD>{},
-                   [&](auto Qc) { issue(std::integral_constant<int, decltype(Qc)::value>{}); });
-    }
-    unroll_seq(std::make_integer_sequence<int, S0_>{}, [&](auto Sc) {
-        constexpr int s = decltype(Sc)::value;
-        constexpr int JB = s / 3 + 1;
-        constexpr int JR = s >= 2 ? (s - 2) / 3 + 1 : 0;
-        step(std::integral_constant<int, s % U>{}, Z{}, std::integral_constant<int, JB>{},
-             std::integral_constant<int, JR>{}, Tt{}, s);
-    });
-    // steady: the last stage of the last wave outputs row y0 + (global step) - 3K + 1
-    if constexpr (LAST) {
-        ry = y0 - 2;
-        st_off = rowoff(ry);
-    }
-    int l = S0_;
-    for (; l + U <= nl; l += U) {
-        unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto Ic) {
-            constexpr int i = decltype(Ic)::value;
-            step(std::integral_constant<int, (S0_ + i) % U>{}, Z{}, Gc{}, Gc{}, Tt{}, l + i);
-        });
-    }
-    unroll_seq(std::make_integer_sequence<int, U - 1>{}, [&](auto Ic) {   // guarded tail
-        constexpr int i = decltype(Ic)::value;
-        if (l + i < nl)
-            step(std::integral_constant<int, (S0_ + i) % U>{}, Z{}, Gc{}, Gc{}, Tt{}, l + i);
-    });
-    // epilogue: local step nl + e runs stages e+1 .. G-1; its ring phase is (nl + e) mod U,
-    // a runtime value here -- dispatch it
-    const int ph = nl % U;
-    unroll_seq(std::make_integer_sequence<int, G - 1>{}, [&](auto Ec) {
-        constexpr int e = decltype(Ec)::value;
-        unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto Pc2) {
-            constexpr int p0 = decltype(Pc2)::value;
-            if (ph == p0)
-                step(std::integral_constant<int, (p0 + e) % U>{},
-                     std::integral_constant<int, e + 1>{}, Gc{}, Gc{}, Ft{}, nl + e);
-        });
-    });
-    if constexpr (FIRST) __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // DMAs landed
-    if constexpr (DIAG) {
-        if (lane == 0 && a.counts) {
-            unsigned long long *d = a.counts + ((size_t)blockIdx.x * NW + W) * 8;
-            d[0] = __builtin_amdgcn_s_memtime() - d_t0;
-            d[1] = d_first;
-            d[2] = d_fw;
-            d[3] = d_nf;
-            d[4] = d_ew;
-            d[5] = d_ne;
-            d[6] = (unsigned long long)nl;
-            d[7] = d_t0;
-        }
-    }
-}
-
-template <int K, int NW, int SYNC = 2, int MINW = 1>
-__global__ __launch_bounds__(64 * NW, MINW) void k_step_wg(const uint64_t *__restrict__ in,
-                                                   uint64_t *__restrict__ out, StepArgs a,
-                                                   int ntx)
-{
-    static_assert(K >= NW, "every wave needs a stage");
-    static_assert(K <= 64, "the edge error must stay inside the halo lanes");
-    __shared__ WgShared sh;
-    const int pipe = blockIdx.x;                         // one band pipeline per workgroup
-    const int tx = pipe % ntx;
-    const int by = pipe / ntx;
-    const int y0 = a.row_lo + by * a.band;
-    if (y0 >= a.row_hi) return;                          // the whole workgroup
-    const int y1 = min(y0 + a.band, a.row_hi);
-    const int nr = max(y1 - y0, K) + 2 * K;              // input rows of the whole pipeline
-    if (threadIdx.x < 4) sh.produced[threadIdx.x] = sh.consumed[threadIdx.x] = 0;
-    __syncthreads();
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    switch (wave) {
-    case 0: wg_wave<K, NW, 0, SYNC>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 1: wg_wave<K, NW, 1, SYNC>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 2: if constexpr (NW > 2) wg_wave<K, NW, 2, SYNC>(in, out, a, sh, tx, y0, y1, nr); break;
-    default: if constexpr (NW > 3) wg_wave<K, NW, 3, SYNC>(in, out, a, sh, tx, y0, y1, nr); break;
-    }
-}
 
 template <int NW, int SYNC, int MINW = 1>
 static void *wg_fn_nw(int turns)
@@ -387,16 +24,16 @@ static void *wg_fn_nw(int turns)
     }
 }
 
-// kMultiWg: 4 waves per band, capped at 64 VGPRs (8 waves per SIMD) where that costs no
-// spills (K <= 12: 65 -> 64; 65536^2 K = 12 38.2 vs 40.0 us/turn uncapped; K >= 13 needs
-// 76+ and spilled 74-285 VGPRs capped); kMultiWgNoBar / kMultiWgDiag: timing ablation /
-// wait diagnostics (tools only)
+// kMultiWg: 4 waves per band, capped where that costs no spills: 64 VGPRs (8 waves per
+// SIMD) at K <= 12 (60 uncapped), 72 (7 waves) at K >= 13 (75 uncapped; 64 spills 28 B);
+// kMultiWgNoBar / kMultiWgDiag: timing ablation / wait diagnostics (tools only)
 static void *wg_fn(int turns, int variant)
 {
     switch (variant) {
     case kMultiWgNoBar: return turns == 8 || turns == 16 ? wg_fn_nw<4, 0>(turns) : nullptr;
     case kMultiWgDiag: return turns == 8 || turns == 16 ? wg_fn_nw<4, 3>(turns) : nullptr;
-    default: return turns >= 13 ? wg_fn_nw<4, 2>(turns) : wg_fn_nw<4, 2, 8>(turns);
+    case kMultiWgHx: return wg_hx_kernel(turns);
+    default: return turns >= 13 ? wg_fn_nw<4, 2, 7>(turns) : wg_fn_nw<4, 2, 8>(turns);
     }
 }
 

@@ -1,0 +1,31 @@
+// gol_wg_hx.hip -- the k_step_wg instantiation table for helix tiling (kMultiWgHx; see HX in
+// gol_wg.h).  Its own translation unit so it compiles in parallel with gol_wg.hip.
+#include "gol_wg.h"
+
+namespace golk {
+
+template <int MINW>
+static void *wg_hx_fn(int turns)
+{
+    switch (turns) {
+    case 4: return reinterpret_cast<void *>(&k_step_wg<4, 4, 2, MINW, true>);
+    case 5: return reinterpret_cast<void *>(&k_step_wg<5, 4, 2, MINW, true>);
+    case 6: return reinterpret_cast<void *>(&k_step_wg<6, 4, 2, MINW, true>);
+    case 7: return reinterpret_cast<void *>(&k_step_wg<7, 4, 2, MINW, true>);
+    case 8: return reinterpret_cast<void *>(&k_step_wg<8, 4, 2, MINW, true>);
+    case 9: return reinterpret_cast<void *>(&k_step_wg<9, 4, 2, MINW, true>);
+    case 10: return reinterpret_cast<void *>(&k_step_wg<10, 4, 2, MINW, true>);
+    case 11: return reinterpret_cast<void *>(&k_step_wg<11, 4, 2, MINW, true>);
+    case 12: return reinterpret_cast<void *>(&k_step_wg<12, 4, 2, MINW, true>);
+    case 13: return reinterpret_cast<void *>(&k_step_wg<13, 4, 2, MINW, true>);
+    case 14: return reinterpret_cast<void *>(&k_step_wg<14, 4, 2, MINW, true>);
+    case 15: return reinterpret_cast<void *>(&k_step_wg<15, 4, 2, MINW, true>);
+    case 16: return reinterpret_cast<void *>(&k_step_wg<16, 4, 2, MINW, true>);
+    default: return nullptr;
+    }
+}
+
+// the register caps of kMultiWg: 8 waves per SIMD at K <= 12 (64 VGPRs), 7 at K >= 13 (72)
+void *wg_hx_kernel(int turns) { return turns >= 13 ? wg_hx_fn<7>(turns) : wg_hx_fn<8>(turns); }
+
+}  // namespace golk
