@@ -215,7 +215,8 @@ __device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[
 // 64 words in order (read back as one ds_read_b64 per lane).
 constexpr bool is_wg_variant(int v)
 {
-    return v == kMultiWg || v == kMultiWgHx || v == kMultiWgNoBar || v == kMultiWgDiag;
+    return v == kMultiWg || v == kMultiWgHx || v == kMultiWgPg || v == kMultiWgNoBar ||
+           v == kMultiWgDiag;
 }
 
 constexpr bool is_il_variant(int v)
@@ -226,6 +227,6 @@ constexpr bool is_il_variant(int v)
 // kernel entry points built in their own translation units (parallel builds)
 void *skew_kernel(int words_per_lane, int turns, int variant);   // gol_skew.hip
 void *wg_kernel(int turns, int variant);                          // gol_wg.hip
-void *wg_hx_kernel(int turns);                                    // gol_wg_hx.hip
+void *wg_hx_kernel(int turns, bool pg);                           // gol_wg_hx.hip
 
 }  // namespace golk

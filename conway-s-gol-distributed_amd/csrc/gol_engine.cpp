@@ -71,6 +71,11 @@ struct gol_ctx {
     long long launches = 0;
     int halo_valid = 0;
     bool blocking_limited = false;           // temporal blocking off: buffer >= 2 GiB
+    // kMultiWgPg: published boundary rows and per-(tile, stage) flags (uncached, grow-only)
+    uint64_t *pg_rows = nullptr;
+    unsigned *pg_flags = nullptr;
+    size_t pg_lanes = 0, pg_tiles = 0;
+    unsigned pg_epoch = 0;
     // control word (gol_set_control): read by gol_step between launches, written by any
     // thread without the engine lock (the reference's CFput flag channel)
     std::atomic<int> control{GOL_CONTROL_RUN};
@@ -197,6 +202,47 @@ int count_now(gol_ctx *c, long long *alive)
     return GOL_OK;
 }
 
+// kMultiWgPg: the published-row scratch and flags for a launch of `a`, grown on demand (the
+// engine's streams are drained first: a running launch may still use the old buffers), and
+// a fresh epoch.  Other variants, and bands the kernel runs as kMultiWgHx, need nothing.
+static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
+{
+    a.xrows = nullptr;
+    a.xflags = nullptr;
+    if (a.multi_variant != golk::kMultiWgPg || !golk::pg_ok(k, a.band)) return hipSuccess;
+    const long long T =
+        golk::multi_pipes(a.width, a.row_hi - a.row_lo, a.band, 2, a.multi_variant);
+    const size_t lanes = (size_t)T * 62 + 64;
+    if (lanes > c->pg_lanes || (size_t)T > c->pg_tiles) {
+        if (2ull * golk::kPgStages * lanes * 8 >= (1ull << 31)) return hipSuccess;   // helix
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess && c->side) e = hipStreamSynchronize(c->side);
+        if (e != hipSuccess) return e;
+        if (c->pg_rows) (void)hipFree(c->pg_rows);
+        if (c->pg_flags) (void)hipFree(c->pg_flags);
+        c->pg_rows = nullptr;
+        c->pg_flags = nullptr;
+        c->pg_lanes = c->pg_tiles = 0;
+        e = hipExtMallocWithFlags((void **)&c->pg_rows, 2ull * golk::kPgStages * lanes * 8,
+                                  hipDeviceMallocUncached);
+        if (e == hipSuccess)
+            e = hipExtMallocWithFlags((void **)&c->pg_flags,
+                                      (size_t)T * golk::kPgStages * sizeof(unsigned),
+                                      hipDeviceMallocUncached);
+        if (e == hipSuccess)
+            e = hipMemset(c->pg_flags, 0, (size_t)T * golk::kPgStages * sizeof(unsigned));
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) return e;
+        c->pg_lanes = lanes;
+        c->pg_tiles = (size_t)T;
+    }
+    a.xrows = c->pg_rows;
+    a.xflags = c->pg_flags;
+    a.xlanes = (unsigned)c->pg_lanes;
+    a.epoch = ++c->pg_epoch;
+    return hipSuccess;
+}
+
 // Create-time timing sweep of the temporal-blocking kernel, its depth K and its band on
 // the engine's own buffers.  The fastest choice depends on grid/residency quantisation and
 // on whether the two boards fit the 256 MiB MALL (tools/sweep.py, tools/strip_emulate.py:
@@ -209,7 +255,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     const long long words = (long long)c->buf_rows * c->pitch;
     if (words < (1ll << 20)) return;                 // < 64 Mi cells: keep the defaults
     std::vector<int> vars{c->multi_variant};
-    if (tune_variant) vars = {golk::kMultiSkewILW16, golk::kMultiWg, golk::kMultiWgHx};
+    if (tune_variant)
+        vars = {golk::kMultiSkewILW16, golk::kMultiWg, golk::kMultiWgHx, golk::kMultiWgPg};
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     struct Cand {
@@ -239,6 +286,10 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                         bands.push_back(b);
                         break;
                     }
+            }
+            if (var == golk::kMultiWgPg) {   // the nearest bands it runs at (golk::pg_ok)
+                for (int &b : bands) b = golk::pg_band(K, b);
+                bands.erase(std::remove(bands.begin(), bands.end(), 0), bands.end());
             }
             std::sort(bands.begin(), bands.end());
             bands.erase(std::unique(bands.begin(), bands.end()), bands.end());
@@ -274,7 +325,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
         for (int rep = 0; rep < reps && ok; ++rep) {
             a.in = c->board[rep & 1];
             a.out = c->board[(rep + 1) & 1];
-            ok = golk::launch_step_multi(a, cd.K, c->stream) == hipSuccess;
+            ok = pg_prepare(c, a, cd.K) == hipSuccess &&
+                 golk::launch_step_multi(a, cd.K, c->stream) == hipSuccess;
         }
         ok = ok && hipEventRecord(e1, c->stream) == hipSuccess &&
              hipEventSynchronize(e1) == hipSuccess;
@@ -468,6 +520,8 @@ void gol_destroy(gol_ctx *c)
         if (c->side) (void)hipStreamSynchronize(c->side);
         if (c->board[0]) (void)hipFree(c->board[0]);
         if (c->board[1]) (void)hipFree(c->board[1]);
+        if (c->pg_rows) (void)hipFree(c->pg_rows);
+        if (c->pg_flags) (void)hipFree(c->pg_flags);
         if (c->blocked) (void)hipFree(c->blocked);
         if (c->counts) (void)hipFree(c->counts);
         if (c->staging) (void)hipFree(c->staging);
@@ -748,6 +802,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
                 if (int rc = wg_diag_launch(c, a, k)) return rc;
             } else if (split && in_lo < in_hi) {
                 golk::StepArgs b = a;
+                // concurrent launches cannot share the published-row scratch
+                if (b.multi_variant == golk::kMultiWgPg) b.multi_variant = golk::kMultiWgHx;
                 b.row_lo = in_lo;
                 b.row_hi = in_hi;
                 HIP_OR_FAIL(c, golk::launch_step_multi(b, k, c->stream));
@@ -760,6 +816,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
                 b.row_hi = a.row_hi;
                 HIP_OR_FAIL(c, golk::launch_step_multi(b, k, c->side));
             } else {
+                HIP_OR_FAIL(c, pg_prepare(c, a, k));
                 HIP_OR_FAIL(c, golk::launch_step_multi(a, k, split ? c->side : c->stream));
             }
             a.band = c->band;

@@ -26,6 +26,11 @@ struct StepArgs {
     int variant;                       // fast-path kernel variant (kVariant*)
     int multi_words;                   // k_step_multi words per lane (1 or 2)
     int multi_variant;                 // temporal-blocking kernel (kMulti*)
+    // kMultiWgPg: boundary rows published between neighbouring bands (engine-owned, uncached)
+    uint64_t *xrows;                   // 2 rows per stage, kPgStages stages, xlanes words each
+    unsigned *xflags;                  // per (tile, stage): epoch of its last publication
+    unsigned xlanes;                   // virtual lanes per published row
+    unsigned epoch;                    // this launch's epoch (above every earlier launch's)
 };
 
 // temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkewILW16 is shipped)
@@ -45,7 +50,10 @@ enum : int {
                             //   lanes (no per-row remainder tile; needs nw even)
     kMultiWgNoBar = 10,     // k_step_wg without hand-off sync: timing ablation (wrong results)
     kMultiWgDiag = 11,      // k_step_wg with per-wave wait timing (tools/wg_diag.py)
-    kMultiCount = 12,
+    kMultiWgPg = 12,        // kMultiWgHx with parallelogram bands: a band's stages take their
+                            //   last 2 input rows from the band below (published through
+                            //   memory) instead of recomputing a 2K-row halo (band >= kPgMinBand)
+    kMultiCount = 13,
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 
@@ -71,6 +79,23 @@ constexpr int kMaxTurnsPerLaunch = 16;
 int multi_max_turns(int variant);       // 16 for kMultiWg, 8 for the k_step_skew variants
 // band height of the boundary launches of an overlapped step (rows next to the halos)
 constexpr int kOverlapBand = 16;
+// kMultiWgPg: stages per tile in the flag array, smallest band; it runs at depths K = 4, 8,
+// 12, 16 (every wave the same stage count) with band = 3K/4 - 5 (mod 6) (its steady loop
+// then ends on a whole unrolled iteration); other launches run as kMultiWgHx
+constexpr int kPgStages = 16;
+constexpr int kPgMinBand = 32;
+constexpr bool pg_ok(int turns, int band)
+{
+    return turns % 4 == 0 && turns <= kPgStages && band >= kPgMinBand &&
+           (band + 5 - 3 * turns / 4) % 6 == 0;
+}
+// the nearest band >= `band` kMultiWgPg runs at depth `turns` (0: none)
+constexpr int pg_band(int turns, int band)
+{
+    for (int b = band < kPgMinBand ? kPgMinBand : band; b < band + 6 + kPgMinBand; ++b)
+        if (pg_ok(turns, b)) return b;
+    return 0;
+}
 bool multi_ok(int width, int turns, int variant);
 // waves sharing one band pipeline (4 for kMultiWg, else 1)
 int multi_waves_per_band(int variant);

@@ -644,7 +644,7 @@ long long multi_tiles(int width, int lane_dwords)
 long long multi_pipes(int width, int rows, int band, int lane_dwords, int variant)
 {
     const long long nb = (rows + band - 1) / band;
-    if (variant == kMultiWgHx) {
+    if (variant == kMultiWgHx || variant == kMultiWgPg) {
         // stored virtual lanes run up to nb (nw + 4) - 3; tile t stores [62t + 1, 62t + 62]
         const long long nwv = (width + 63) / 64 + 4;
         return (nb * nwv - 3 + 61) / 62;
@@ -675,9 +675,12 @@ bool multi_fits(int nw, int pitch, int rows)
 
 // k_step_wg: one workgroup (4 waves) per (tile, band) pipeline; depths 2, 3 run on
 // k_step_skew (same interleaved layout and tiles)
-static hipError_t launch_wg(const StepArgs &a, int turns, hipStream_t s)
+static hipError_t launch_wg(const StepArgs &a0, int turns, hipStream_t s)
 {
-    const bool hx = a.multi_variant == kMultiWgHx;
+    StepArgs a = a0;                                    // other shapes / no scratch: helix
+    if (a.multi_variant == kMultiWgPg && (!pg_ok(turns, a.band) || !a.xrows || !a.xflags))
+        a.multi_variant = kMultiWgHx;
+    const bool hx = a.multi_variant == kMultiWgHx || a.multi_variant == kMultiWgPg;
     const long long blocks =
         multi_pipes(a.width, a.row_hi - a.row_lo, a.band, 2, a.multi_variant);
     // band tiling: tiles per band; helix: the tile count itself (blockIdx.x = tile)

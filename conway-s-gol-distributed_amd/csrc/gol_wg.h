@@ -50,11 +50,14 @@ constexpr int kWgR = 6;                                 // hand-off ring slots p
 constexpr int kWgSpinLimit = 1 << 22;
 constexpr int kWgLag = 3;                               // SYNC 2: consumer's initial lag (rows)
 
-template <int NW>
+template <int NW, bool PG = false>
 struct WgShared {
     uint32_t dma[kWgRQ][128];                           // wave 0's input rows (64 words each)
     uint32_t xfer[NW - 1][kWgR][128];                   // wave w -> w+1 rows
     uint32_t produced[NW], consumed[NW];                // per boundary: rows written / read
+    // PG: each wave's rows from below, 2 stages at a time (stage j in slot j % 2): 8 KB, not
+    // 16, keeps 7 workgroups (of K = 16) per CU
+    uint32_t nb[PG ? NW : 1][PG ? 2 : 1][2][128];
 };
 
 __device__ __forceinline__ uint32_t lds_load_counter(const uint32_t *p)
@@ -87,10 +90,25 @@ __device__ __forceinline__ void lds_store_counter(uint32_t *p, uint32_t v)
 // error); word pairs stay 16-B aligned (nw even, bands of even length), so the 16-B DMA
 // still works.  Stored fraction 256/260 x 62/64 = 95 % at 16384^2, and any band height
 // gives a full grid (the last band may be short: its lanes mask their stores).
-template <int K, int NW, int W, int SYNC, bool HX>
+// PG (kMultiWgPg, helix only): parallelogram bands.  With the trapezoid above, stage j of a
+// band recomputes 2(K-1-j) rows of its neighbours' outputs (a 2K-row halo: 16384^2, K = 16,
+// 68-row bands: 84 stage rows per 68 output rows).  Here stage j of band m outputs exactly
+// its rows [y0 - K + 1 + j, y1 - K + 1 + j) -- the region slides down one row per stage, so
+// the bands of one stage still partition the board -- and takes the last 2 of its band + 2
+// input rows from stage j-1 of band m+1, whose FIRST 2 output rows they are.  So each
+// stage publishes its first 2 output rows (e = 0, 1) to memory early in the pipeline and
+// substitutes the 2 rows published by the band below for its own outputs e = band, band+1
+// near the end (its computed ones would need rows it does not have).  Tiles run in reverse
+// order (blockIdx 0 = the last tile), and a tile only waits for tiles after it, which were
+// dispatched first and wait for nothing before publishing: no deadlock at any occupancy.
+// The band of the last block (and every tile holding some of its lanes) keeps the
+// trapezoid: it breaks the torus cycle and, in strips, ends at the halo.  Published rows
+// and flags live in uncached memory (hipDeviceMallocUncached): visible across the XCDs'
+// L2s without cache maintenance.  Flags carry the launch epoch, so they are never reset.
+template <int K, int NW, int W, int SYNC, bool HX, bool PG = false>
 __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
-                                        const StepArgs &a, WgShared<NW> &sh, int tx, int y0, int y1,
-                                        int nr)
+                                        const StepArgs &a, WgShared<NW, PG> &sh, int tx, int y0,
+                                        int y1, int nr, bool trap, int ntx)
 {
     constexpr int ND = 2;
     constexpr int G = WgSplit<K, NW>::G(W);
@@ -104,7 +122,9 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     constexpr int STRIDE = 62 * ND, SHIFT = ND;
     static_assert(NW >= 2 && NW <= 8 && G >= 1, "2..8 waves, every wave a stage");
     const int lane = threadIdx.x & 63;
-    const int nl = nr - 2 * J;                           // rows this wave's first stage takes
+    const bool pgt = PG && !trap;                        // parallelogram tile
+    // rows this wave's first stage takes, rows it hands on
+    const int nl = pgt ? nr : nr - 2 * J;
 
     const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
     const int M = a.modrows;
@@ -117,6 +137,11 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     bool st;
     uint32_t lane_b, lane_dma;
     int hy0 = 0, hh = 0, hy0d = 0;                       // HX: lane's band start / height, DMA lane's
+    // PG: publishing lane / lane taking rows from below, their byte offsets in a published row,
+    // the tiles that publish this tile's rows from below
+    bool pub_ok = false, sub_ok = false;
+    uint32_t pub_b = 0, cons_b = 0;
+    int t_a = 0, t_b = -1;
     if constexpr (HX) {
         const int nwv = a.nw + 4;
         const int nblk = (a.row_hi - a.row_lo + a.band - 1) / a.band;
@@ -141,6 +166,17 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
         hy0 = a.row_lo + m * a.band;
         hh = min(a.band, a.row_hi - hy0);
         hy0d = a.row_lo + md * a.band;
+        if constexpr (PG) {
+            const int u = 62 * tx + lane;                // virtual lane (interior ones publish)
+            pub_ok = lane >= 1 && lane < 63 && u < nblk * nwv;
+            pub_b = (uint32_t)u * 8u;
+            // every lane of a band with a band below -- halo lanes too: they have no rows
+            // past the band either, and feed the stored lanes' last rows
+            sub_ok = m < nblk - 1;
+            cons_b = (uint32_t)(62 * tx + 2 * (lane & 31) + nwv) * 8u;   // 16-B DMA pairs
+            t_a = (62 * tx + nwv - 1) / 62;              // publisher of u: (u - 1) / 62
+            t_b = min((62 * tx + nwv + 62) / 62, ntx - 1);
+        }
     } else {
         const int nd = 2 * a.nw;
         const int t0 = tx * STRIDE + SHIFT;
@@ -227,7 +263,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
             }
         }
     };
-    const int nemit = nl - 2 * G;                        // rows the downstream wave takes
+    const int nemit = pgt ? nl : nl - 2 * G;             // rows the downstream wave takes
     auto emit = [&](auto SMc, int q, const uint32_t (&o)[ND]) {   // non-last waves: row q
         constexpr int SM = decltype(SMc)::value;
         constexpr int slot = ((SM - EMIT0) % R + R) % R;
@@ -291,26 +327,102 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
         }
     };
 
-    // local step l (SM = l mod U): local stages [JA, JB) active, stages < JR apply the rule
-    auto step = [&](auto SMc, auto JAc, auto JBc, auto JRc, auto LDc, int l) {
+    // PG: stage jl's output e = l - 3 jl - 2 (its first rule step is 3 jl + 2).  Its outputs
+    // e = 0, 1 are published (steps 3 jl + 2, 3 jl + 3: prologue or the peeled first steady
+    // iteration, compile-time); its outputs e = band, band + 1 are the rows of the band below
+    // (steps band + 3 jl + 2, + 3: the epilogue, compile-time -- the host runs PG only with
+    // band + 2 = S0_ mod U, so the steady loop ends exactly at step band + 2).  The global
+    // last stage does neither: its rows are the launch's output.
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)a.xrows, (short)0, PG ? (int)(2u * kPgStages * a.xlanes * 8u) : 0, kBufFlags);
+    auto rowb = [&](int jg, int r) -> uint32_t { return (uint32_t)(2 * jg + r) * a.xlanes * 8u; };
+    constexpr int NS = (J + G <= K - 1) ? G : G - 1;     // PG: stages that publish / take
+    constexpr int XPUB = 1 << 16;                        // step flags: publish e = 0, 1;
+    // bits 0..7 / 8..15: stage j's output this step is row 0 / 1 from below
+    auto publish = [&](auto Jc, int l, const uint32_t (&o)[ND]) {
+        constexpr int jl = decltype(Jc)::value;
+        if constexpr (PG && jl < NS) {
+            const int e = l - 3 * jl - 2;                // a constant in the steps that publish
+            if ((e == 0 || e == 1) && pub_ok) buf_store(o, rx, pub_b, rowb(J + jl, e));
+        }
+    };
+    // once per wave, after its last publication store (stage G-1's e = 1, step 3G): the flags
+    auto publish_flags = [&]() {
+        if constexpr (PG && NS > 0) {
+            __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // the stores are done
+            if (lane == 0)
+                for (int jl = 0; jl < NS; ++jl)
+                    __hip_atomic_store(&a.xflags[tx * kPgStages + J + jl], a.epoch,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    // stage jl's 2 rows from below into LDS slot jl % 2 (16-B DMA from lanes 0..31)
+    auto nb_load = [&](int jl) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        // (device pass only: clang's host pass rejects the second kernel instantiating this
+        // wave body -- a deferred-diagnostic quirk -- and the host never runs it)
+        if constexpr (PG)
+            if (lane < 32)
+                for (int r = 0; r < 2; ++r)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rx, (lds_void *)&sh.nb[W][jl & 1][r][0], 16, cons_b, rowb(J + jl, r), 0, 0);
+#endif
+    };
+    // once per wave, a few steps before the first substitution: wait for the tiles below and
+    // pull the rows of the first 2 stages into LDS (the epilogue loads the others)
+    auto take_rows = [&]() {
+        if constexpr (PG && NS > 0) {
+            for (int jl = 0; jl < NS; ++jl)
+                for (int t = t_a; t <= t_b; ++t) {
+                    unsigned *f = &a.xflags[t * kPgStages + J + jl];
+                    for (int spin = 0; spin < kWgSpinLimit; ++spin) {
+                        const unsigned v = (unsigned)__builtin_amdgcn_readfirstlane((int)
+                            __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        if (v == a.epoch) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+            for (int jl = 0; jl < NS && jl < 2; ++jl) nb_load(jl);
+            __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // rows landed
+        }
+    };
+
+    // local step l (SM = l mod U): local stages [JA, JB) active, stages < JR apply the rule;
+    // XF: PG flags (XPUB, substitution masks)
+    auto step = [&](auto SMc, auto JAc, auto JBc, auto JRc, auto LDc, int l, auto XFc) {
         constexpr int SM = decltype(SMc)::value;
         constexpr int P = SM % 3;
         constexpr int JA = decltype(JAc)::value, JB = decltype(JBc)::value;
         constexpr int JR = decltype(JRc)::value;
+        constexpr int XF = decltype(XFc)::value;
         using Pc = std::integral_constant<int, P>;
         unroll_seq(std::make_integer_sequence<int, JB - JA>{}, [&](auto I) {
             constexpr int j = JB - 1 - decltype(I)::value;
             using RULE = std::integral_constant<bool, (j < JR)>;
+            constexpr int SUBR = (XF >> j) & 1 ? 0 : (XF >> (8 + j)) & 1 ? 1 : -1;
             uint32_t x[ND];
-            if constexpr (j == 0) {
-                fetch(SMc, l, x);
-            } else {
+            if constexpr (SUBR < 0) {
+                if constexpr (j == 0) {
+                    fetch(SMc, l, x);
+                } else {
 #pragma unroll
-                for (int k = 0; k < ND; ++k) x[k] = XS[j][k];
+                    for (int k = 0; k < ND; ++k) x[k] = XS[j][k];
+                }
             }
             if constexpr (j == G - 1) {
                 uint32_t o[ND];
-                stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, o);
+                if constexpr (SUBR >= 0) {
+                    if (pgt) {                           // (trapezoid tiles: past their end)
+                        o[0] = sh.nb[W][j & 1][SUBR][2 * lane];
+                        o[1] = sh.nb[W][j & 1][SUBR][2 * lane + 1];
+                    } else {
+                        o[0] = o[1] = 0;
+                    }
+                } else {
+                    stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, o);
+                    if constexpr (RULE::value && (XF & XPUB) != 0)
+                        publish(std::integral_constant<int, j>{}, l, o);
+                }
                 if constexpr (RULE::value) {
                     if constexpr (LAST) {
                         if constexpr (HX) {
@@ -324,22 +436,31 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
                         emit(SMc, l - EMIT0, o);
                     }
                 }
+            } else if constexpr (SUBR >= 0) {
+                if (pgt) {
+                    XS[j + 1][0] = sh.nb[W][j & 1][SUBR][2 * lane];
+                    XS[j + 1][1] = sh.nb[W][j & 1][SUBR][2 * lane + 1];
+                }
             } else {
                 stage(std::integral_constant<int, j>{}, Pc{}, RULE{}, x, XS[j + 1]);
+                if constexpr (RULE::value && (XF & XPUB) != 0)
+                    publish(std::integral_constant<int, j>{}, l, XS[j + 1]);
             }
-#ifdef GOL_WG_SCHED_BARRIER
-            __builtin_amdgcn_sched_barrier(0);
-#endif
         });
         if constexpr (FIRST && decltype(LDc)::value) issue(std::integral_constant<int, (SM + PD) % RQ>{});
         if constexpr (LAST && JR == G) {
             adv(st_off);
             ++ry;
         }
+        if constexpr (PG && (XF & XPUB) != 0)
+            if (l == 3 * G) publish_flags();
     };
     using Tt = std::true_type;
+    using Ft = std::false_type;
     using Z = std::integral_constant<int, 0>;
     using Gc = std::integral_constant<int, G>;
+    using XP = std::integral_constant<int, PG ? XPUB : 0>;
+    using X0 = std::integral_constant<int, 0>;
 
     if constexpr (FIRST) {
         if constexpr (HX) ld_off = lane_dma + rowoff(hy0d - K);
@@ -352,7 +473,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
         constexpr int JB = s / 3 + 1;
         constexpr int JR = s >= 2 ? (s - 2) / 3 + 1 : 0;
         step(std::integral_constant<int, s % U>{}, Z{}, std::integral_constant<int, JB>{},
-             std::integral_constant<int, JR>{}, Tt{}, s);
+             std::integral_constant<int, JR>{}, Tt{}, s, XP{});
     });
     // steady: the last stage of the last wave outputs row y0 + (global step) - 3K + 1
     if constexpr (LAST) {
@@ -373,12 +494,60 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     // exit: a guarded tail plus an epilogue dispatched on the runtime phase nl mod U kept
     // all three window slots of every stage live across the loop (K = 16: 92 instead of 74
     // VGPRs, 5 instead of 6 waves/SIMD; K = 12: 71 vs 63, 7 vs 8).
-    const int l_end = nl + G - 1;
-    for (int l = S0_; l < l_end; l += U) {
+    // PG: the first steady iteration is peeled (it holds the last publications and the flag
+    // step 3G).  A parallelogram tile's loop then ends at step band + 2 (a multiple of U
+    // past S0_, by the host's choice of band), with the wave's rows from below taken in the
+    // iteration holding step band - 3, and the epilogue's step ep (local step band + 2 + ep)
+    // substitutes stage ep / 3's output row ep % 3 (ep % 3 < 2) and runs the stages above
+    // it.  A trapezoid tile (last band) runs the padded loop without substitutions.
+    int l0 = S0_;
+    if constexpr (PG) {
         unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto Ic) {
             constexpr int i = decltype(Ic)::value;
-            step(std::integral_constant<int, (S0_ + i) % U>{}, Z{}, Gc{}, Gc{}, Tt{}, l + i);
+            step(std::integral_constant<int, (S0_ + i) % U>{}, Z{}, Gc{}, Gc{}, Tt{}, S0_ + i,
+                 XP{});
         });
+        l0 = S0_ + U;
+    }
+    if constexpr (PG) {
+        // one loop + epilogue for both tile kinds (two alternative loops in one kernel cost
+        // 129 VGPRs against 79 and 75 apart).  A trapezoid tile ends its loop once stage 0
+        // is done (L >= nl) and skips the substitutions: the epilogue step that would
+        // substitute stage js comes after its last needed output there.
+        const int L = pgt ? a.band + 2 : S0_ + U + (max(nl - S0_ - U, 0) + U - 1) / U * U;
+        const int pf = pgt ? a.band - 3 : -1;
+        for (int l = l0; l < L; l += U) {
+            if (pf >= l && pf < l + U) take_rows();
+            unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto Ic) {
+                constexpr int i = decltype(Ic)::value;
+                step(std::integral_constant<int, (S0_ + i) % U>{}, Z{}, Gc{}, Gc{}, Tt{}, l + i,
+                     X0{});
+            });
+        }
+        if (pgt && pf < l0) take_rows();
+        constexpr int GS = LAST ? G - 1 : G;             // stages that substitute
+        unroll_seq(std::make_integer_sequence<int, 3 * G - 1>{}, [&](auto Ec) {
+            constexpr int ep = decltype(Ec)::value;
+            constexpr int js = ep / 3, r = ep % 3;
+            constexpr int XF = (js < GS && r < 2) ? (1 << (js + 8 * r)) : 0;
+            // stage js >= 2: its rows were loaded 4 steps ago into the slot stage js - 2 freed
+            if constexpr (r == 0 && js >= 2 && js < NS)
+                __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+            step(std::integral_constant<int, (S0_ + ep) % U>{},
+                 std::integral_constant<int, (ep + 1) / 3>{}, Gc{}, Gc{}, Ft{}, L + ep,
+                 std::integral_constant<int, XF>{});
+            if constexpr (r == 2 && js + 2 < NS)
+                if (pgt) nb_load(js + 2);
+        });
+    } else {
+        const int l_end = nl + G - 1;
+        for (int l = l0; l < l_end; l += U) {
+            unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto Ic) {
+                constexpr int i = decltype(Ic)::value;
+                step(std::integral_constant<int, (S0_ + i) % U>{}, Z{}, Gc{}, Gc{}, Tt{}, l + i,
+                     X0{});
+            });
+        }
     }
     if constexpr (FIRST) __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // DMAs landed
     if constexpr (DIAG) {
@@ -396,34 +565,42 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     }
 }
 
-template <int K, int NW, int SYNC = 2, int MINW = 1, bool HX = false>
+template <int K, int NW, int SYNC = 2, int MINW = 1, bool HX = false, bool PG = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_step_wg(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, StepArgs a,
                                                    int ntx)
 {
     static_assert(K >= NW, "every wave needs a stage");
     static_assert(K <= 64, "the edge error must stay inside the halo lanes");
-    __shared__ WgShared<NW> sh;
+    static_assert(!PG || (HX && K <= kPgStages && K <= 4 * NW), "PG: helix, <= 4 stages a wave");
+    __shared__ WgShared<NW, PG> sh;
     const int pipe = blockIdx.x;                         // one band pipeline per workgroup
-    // HX: one helix tile per workgroup (ntx = the tile count), every lane its own band
-    const int tx = HX ? pipe : pipe % ntx;
+    // HX: one helix tile per workgroup (ntx = the tile count), every lane its own band;
+    // PG: the last tile first
+    const int tx = HX ? (PG ? ntx - 1 - pipe : pipe) : pipe % ntx;
     const int by = HX ? 0 : pipe / ntx;
     const int y0 = a.row_lo + by * a.band;
     if (HX ? pipe >= ntx : y0 >= a.row_hi) return;       // the whole workgroup
     const int y1 = min(y0 + a.band, a.row_hi);
-    const int nr = max(y1 - y0, K) + 2 * K;              // input rows of the whole pipeline
+    // PG: tiles holding lanes of the last band run the trapezoid (band + 2K input rows)
+    bool trap = true;
+    if constexpr (PG) {
+        const int nblk = (a.row_hi - a.row_lo + a.band - 1) / a.band;
+        trap = (62 * tx + 63) / (a.nw + 4) >= nblk - 1;
+    }
+    const int nr = trap ? max(y1 - y0, K) + 2 * K : a.band + 2;   // input rows of the pipeline
     if (threadIdx.x < NW) sh.produced[threadIdx.x] = sh.consumed[threadIdx.x] = 0;
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     switch (wave) {
-    case 0: wg_wave<K, NW, 0, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 1: wg_wave<K, NW, 1, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 2: if constexpr (NW > 2) wg_wave<K, NW, 2, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 3: if constexpr (NW > 3) wg_wave<K, NW, 3, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 4: if constexpr (NW > 4) wg_wave<K, NW, 4, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 5: if constexpr (NW > 5) wg_wave<K, NW, 5, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
-    case 6: if constexpr (NW > 6) wg_wave<K, NW, 6, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
-    default: if constexpr (NW > 7) wg_wave<K, NW, 7, SYNC, HX>(in, out, a, sh, tx, y0, y1, nr); break;
+    case 0: wg_wave<K, NW, 0, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 1: wg_wave<K, NW, 1, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 2: if constexpr (NW > 2) wg_wave<K, NW, 2, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 3: if constexpr (NW > 3) wg_wave<K, NW, 3, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 4: if constexpr (NW > 4) wg_wave<K, NW, 4, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 5: if constexpr (NW > 5) wg_wave<K, NW, 5, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 6: if constexpr (NW > 6) wg_wave<K, NW, 6, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    default: if constexpr (NW > 7) wg_wave<K, NW, 7, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
     }
 }
 

@@ -32,7 +32,8 @@ static void *wg_fn(int turns, int variant)
     switch (variant) {
     case kMultiWgNoBar: return turns == 8 || turns == 16 ? wg_fn_nw<4, 0>(turns) : nullptr;
     case kMultiWgDiag: return turns == 8 || turns == 16 ? wg_fn_nw<4, 3>(turns) : nullptr;
-    case kMultiWgHx: return wg_hx_kernel(turns);
+    case kMultiWgHx: return wg_hx_kernel(turns, false);
+    case kMultiWgPg: return wg_hx_kernel(turns, true);
     default: return turns >= 13 ? wg_fn_nw<4, 2, 7>(turns) : wg_fn_nw<4, 2, 8>(turns);
     }
 }

@@ -4,28 +4,32 @@
 
 namespace golk {
 
-template <int MINW>
+template <int MINW, bool PG>
 static void *wg_hx_fn(int turns)
 {
     switch (turns) {
-    case 4: return reinterpret_cast<void *>(&k_step_wg<4, 4, 2, MINW, true>);
-    case 5: return reinterpret_cast<void *>(&k_step_wg<5, 4, 2, MINW, true>);
-    case 6: return reinterpret_cast<void *>(&k_step_wg<6, 4, 2, MINW, true>);
-    case 7: return reinterpret_cast<void *>(&k_step_wg<7, 4, 2, MINW, true>);
-    case 8: return reinterpret_cast<void *>(&k_step_wg<8, 4, 2, MINW, true>);
-    case 9: return reinterpret_cast<void *>(&k_step_wg<9, 4, 2, MINW, true>);
-    case 10: return reinterpret_cast<void *>(&k_step_wg<10, 4, 2, MINW, true>);
-    case 11: return reinterpret_cast<void *>(&k_step_wg<11, 4, 2, MINW, true>);
-    case 12: return reinterpret_cast<void *>(&k_step_wg<12, 4, 2, MINW, true>);
-    case 13: return reinterpret_cast<void *>(&k_step_wg<13, 4, 2, MINW, true>);
-    case 14: return reinterpret_cast<void *>(&k_step_wg<14, 4, 2, MINW, true>);
-    case 15: return reinterpret_cast<void *>(&k_step_wg<15, 4, 2, MINW, true>);
-    case 16: return reinterpret_cast<void *>(&k_step_wg<16, 4, 2, MINW, true>);
+    case 4: return reinterpret_cast<void *>(&k_step_wg<4, 4, 2, MINW, true, PG>);
+    case 5: return reinterpret_cast<void *>(&k_step_wg<5, 4, 2, MINW, true, PG>);
+    case 6: return reinterpret_cast<void *>(&k_step_wg<6, 4, 2, MINW, true, PG>);
+    case 7: return reinterpret_cast<void *>(&k_step_wg<7, 4, 2, MINW, true, PG>);
+    case 8: return reinterpret_cast<void *>(&k_step_wg<8, 4, 2, MINW, true, PG>);
+    case 9: return reinterpret_cast<void *>(&k_step_wg<9, 4, 2, MINW, true, PG>);
+    case 10: return reinterpret_cast<void *>(&k_step_wg<10, 4, 2, MINW, true, PG>);
+    case 11: return reinterpret_cast<void *>(&k_step_wg<11, 4, 2, MINW, true, PG>);
+    case 12: return reinterpret_cast<void *>(&k_step_wg<12, 4, 2, MINW, true, PG>);
+    case 13: return reinterpret_cast<void *>(&k_step_wg<13, 4, 2, MINW, true, PG>);
+    case 14: return reinterpret_cast<void *>(&k_step_wg<14, 4, 2, MINW, true, PG>);
+    case 15: return reinterpret_cast<void *>(&k_step_wg<15, 4, 2, MINW, true, PG>);
+    case 16: return reinterpret_cast<void *>(&k_step_wg<16, 4, 2, MINW, true, PG>);
     default: return nullptr;
     }
 }
 
 // the register caps of kMultiWg: 8 waves per SIMD at K <= 12 (64 VGPRs), 7 at K >= 13 (72)
-void *wg_hx_kernel(int turns) { return turns >= 13 ? wg_hx_fn<7>(turns) : wg_hx_fn<8>(turns); }
+void *wg_hx_kernel(int turns, bool pg)
+{
+    if (pg) return turns >= 13 ? wg_hx_fn<7, true>(turns) : wg_hx_fn<8, true>(turns);
+    return turns >= 13 ? wg_hx_fn<7, false>(turns) : wg_hx_fn<8, false>(turns);
+}
 
 }  // namespace golk
