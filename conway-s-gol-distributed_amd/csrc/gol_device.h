@@ -213,12 +213,6 @@ __device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[
 // 4-B DMAs from all lanes.  Tiles start one word later (lane 0 holds an even word, so no
 // pair straddles the row's wrap; the last tile stores word 0), and the slot holds the row's
 // 64 words in order (read back as one ds_read_b64 per lane).
-constexpr bool is_wg_variant(int v)
-{
-    return v == kMultiWg || v == kMultiWgHx || v == kMultiWgPg || v == kMultiWgNoBar ||
-           v == kMultiWgDiag;
-}
-
 constexpr bool is_il_variant(int v)
 {
     return v == kMultiSkewIL || v == kMultiSkewILW16 || is_wg_variant(v);
@@ -228,5 +222,7 @@ constexpr bool is_il_variant(int v)
 void *skew_kernel(int words_per_lane, int turns, int variant);   // gol_skew.hip
 void *wg_kernel(int turns, int variant);                          // gol_wg.hip
 void *wg_hx_kernel(int turns, bool pg);                           // gol_wg_hx.hip
+void *wg_deep_kernel_a(int turns);                                // gol_wg_deep_a.hip (17..24)
+void *wg_deep_kernel_b(int turns);                                // gol_wg_deep_b.hip (25..32)
 
 }  // namespace golk

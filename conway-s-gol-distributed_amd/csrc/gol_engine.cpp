@@ -50,7 +50,9 @@ struct gol_ctx {
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
     int multi_words = 2;                     // k_step_multi words per lane
     int multi_variant = golk::kMultiSkewILW16;  // temporal-blocking kernel (kMulti*)
-    int band_multi = 64;                     // band height of the multi-turn kernel
+    int band_multi = 64;                     // band height of the multi-turn kernel (depth tpl)
+    int band_at[golk::kMaxTurnsPerLaunch + 1] = {};   // band_for_depth cache (0 = not yet)
+    int ncu = 0;                             // compute units of the device
     float tuned_us_per_turn = 0.f;           // autotune's best measurement (0 = not tuned)
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
@@ -180,6 +182,41 @@ int launch_depth(const gol_ctx *c, int64_t room)
     return golk::multi_ok(c->cfg.width, k, c->multi_variant) ? k : 1;
 }
 
+// Band height of a launch of depth k.  band_multi was chosen (tuned) for depth tpl; a
+// launch of another depth -- the even split's shallower launches, a short gol_step, the last
+// block before a halo exchange -- runs a kernel with another residency (k_step_wg: 4..8 waves
+// per workgroup at 7 or 8 waves per SIMD; k_step_skew: 2..4 waves per SIMD), where that band
+// would leave resident slots idle or spill a few pipelines into one more round (65536^2:
+// K = 16's band 607 fills 1791 of 1792 slots; a K = 20 launch has 1280).  Keep the tuned
+// number of rounds instead: the smallest band whose grid fits them at depth k (kMultiWgPg:
+// the next band it runs at).  A band the caller fixed (gol_config.band_rows) is kept.
+int band_for_depth(gol_ctx *c, int k)
+{
+    if (k == c->tpl || c->cfg.band_rows > 0 || k < 2 || k > golk::kMaxTurnsPerLaunch)
+        return c->band_multi;
+    int &b = c->band_at[k];
+    if (b > 0) return b;
+    b = c->band_multi;
+    const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
+    const int per = golk::multi_pipes_per_block(c->multi_variant);
+    const long long cap_t =
+        (long long)c->ncu * golk::multi_blocks_per_cu(c->tpl, c->multi_words, c->multi_variant) * per;
+    const long long cap_k =
+        (long long)c->ncu * golk::multi_blocks_per_cu(k, c->multi_words, c->multi_variant) * per;
+    if (cap_t <= 0 || cap_k <= 0) return b;
+    const int W = c->cfg.width, rows = c->buf_rows;
+    const long long pipes = golk::multi_pipes(W, rows, c->band_multi, lane_dw, c->multi_variant);
+    const long long rounds = std::max(1ll, (pipes + cap_t - 1) / cap_t);
+    for (int band = 16; band <= std::max(rows, 16); ++band)
+        if (golk::multi_pipes(W, rows, band, lane_dw, c->multi_variant) <= rounds * cap_k) {
+            b = band;
+            break;
+        }
+    if (c->multi_variant == golk::kMultiWgPg && golk::pg_ok(k, golk::pg_band(k, b)))
+        b = golk::pg_band(k, b);
+    return b;
+}
+
 // the word layout a launch of depth k runs on
 bool stepping_il(const gol_ctx *c, int k)
 {
@@ -265,8 +302,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     std::vector<Cand> cand;
     for (int var : vars) {
         // K = 7 measured no faster than 6 / 8 on k_step_skew (DESIGN); k_step_wg goes to 16
-        std::vector<int> ks = golk::multi_waves_per_band(var) > 1 ? std::vector<int>{8, 12, 16}
-                                                            : std::vector<int>{6, 8, 10};
+        std::vector<int> ks = !golk::is_wg_variant(var) ? std::vector<int>{6, 8, 10}
+                                                  : std::vector<int>{8, 12, 16};
         if (!tune_k) ks = {c->tpl};
         static const int kBands[] = {16, 20, 24, 32, 40, 48, 64, 96, 137, 192};
         const int lane_dw = golk::multi_lane_dwords(c->multi_words, var);
@@ -352,6 +389,11 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     float best = 0.f;
     for (size_t i = 0; i < cand.size(); ++i)
         if (t[i] > 0.f && (best == 0.f || t[i] < best)) best = t[i];
+    if (getenv("GOL_AUTOTUNE_LOG"))   // tools only: the measured table on stderr
+        for (size_t i = 0; i < cand.size(); ++i)
+            fprintf(stderr, "autotune %dx%d var=%d K=%d band=%d us_per_turn=%.3f reps=%d\n",
+                    c->cfg.width, c->buf_rows, cand[i].var, cand[i].K, cand[i].band,
+                    t[i] * 1000.f, reps);
     // within 1.5 % of the best, the deepest K wins: the same steady rate with fewer launches
     // when a run is short (65536^2, 20 turns: K = 10 -> 2 launches, 104.7k GCUPS; K = 8 ->
     // 7 + 7 + 6, 100.8k; steady state 36.0 vs 36.2 us/turn)
@@ -371,6 +413,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     c->multi_variant = pick.var;
     c->tpl = pick.K;
     c->band_multi = pick.band;
+    for (int &b : c->band_at) b = 0;
     c->tuned_us_per_turn = best * 1000.f;
 }
 
@@ -451,7 +494,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     }
     const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
     const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
-    const bool wg = golk::multi_waves_per_band(c->multi_variant) > 1;
+    const bool wg = golk::is_wg_variant(c->multi_variant);
     c->tpl = cfg->turns_per_launch > 0 ? cfg->turns_per_launch
                                        : (wg ? 16 : (auto_bm >= 48 ? 8 : 6));
     if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) c->tpl = atoi(v);
@@ -462,10 +505,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     c->halo_valid = cfg->halo;
 
     DeviceGuard g(dev);
+    (void)hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, dev);
     c->band_multi = cfg->band_rows;
     if (c->band_multi <= 0 && c->tpl > 1) {
-        int ncu = 0;
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int ncu = c->ncu;
         const int bpc = golk::multi_blocks_per_cu(c->tpl, c->multi_words, c->multi_variant);
         c->band_multi = golk::pick_band_multi(cfg->width, cfg->rows, lane_dw, c->tpl,
                                               ncu * bpc *
@@ -678,7 +721,7 @@ int wg_diag_launch(gol_ctx *c, golk::StepArgs a, int k)
 {
     const long long ntx = golk::multi_tiles(c->cfg.width, 2);
     const long long pipes = ntx * ((a.row_hi - a.row_lo + a.band - 1) / a.band);
-    const size_t n = (size_t)pipes * 4 * 8;
+    const size_t n = (size_t)pipes * 4 * 10;
     unsigned long long *d = nullptr;
     HIP_OR_FAIL(c, hipMalloc(&d, n * 8));
     HIP_OR_FAIL(c, hipMemsetAsync(d, 0, n * 8, c->stream));
@@ -689,16 +732,31 @@ int wg_diag_launch(gol_ctx *c, golk::StepArgs a, int k)
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     (void)hipFree(d);
     unsigned long long t0min = ~0ull, t1max = 0;
+    std::vector<unsigned long long> starts, ends;        // wave 0's start / wave 3's end
     for (long long p = 0; p < pipes; ++p)
         for (int w = 0; w < 4; ++w) {
-            const unsigned long long *e = &h[((size_t)p * 4 + w) * 8];
-            t0min = std::min(t0min, e[7]);
-            t1max = std::max(t1max, e[7] + e[0]);
+            const unsigned long long *e = &h[((size_t)p * 4 + w) * 10];
+            if (e[8] == 0) continue;                     // a workgroup past the last band
+            t0min = std::min(t0min, e[8]);
+            t1max = std::max(t1max, e[9]);
+            if (w == 0) starts.push_back(e[8]);
+            if (w == 3) ends.push_back(e[9]);
         }
+    auto pct = [](std::vector<unsigned long long> v, unsigned long long base, double q) {
+        if (v.empty()) return 0.0;
+        std::sort(v.begin(), v.end());
+        return (double)(v[(size_t)(q * (double)(v.size() - 1))] - base);
+    };
+    fprintf(stderr,
+            "wg_diag starts (100 MHz ticks after the first) p10 %.0f p50 %.0f p90 %.0f max %.0f; "
+            "ends p10 %.0f p50 %.0f p90 %.0f max %.0f\n",
+            pct(starts, t0min, 0.1), pct(starts, t0min, 0.5), pct(starts, t0min, 0.9),
+            pct(starts, t0min, 1.0), pct(ends, t0min, 0.1), pct(ends, t0min, 0.5),
+            pct(ends, t0min, 0.9), pct(ends, t0min, 1.0));
     for (int w = 0; w < 4; ++w) {
         double life = 0, first = 0, fw = 0, nf = 0, ew = 0, ne = 0, nl = 0;
         for (long long p = 0; p < pipes; ++p) {
-            const unsigned long long *e = &h[((size_t)p * 4 + w) * 8];
+            const unsigned long long *e = &h[((size_t)p * 4 + w) * 10];
             life += (double)e[0]; first += (double)e[1]; fw += (double)e[2];
             nf += (double)e[3]; ew += (double)e[4]; ne += (double)e[5]; nl += (double)e[6];
         }
@@ -708,7 +766,7 @@ int wg_diag_launch(gol_ctx *c, golk::StepArgs a, int k)
                 k, a.band, pipes, w, life / pipes, 100 * first / life, 100 * fw / life, nf / nl,
                 100 * ew / life, ne / nl);
     }
-    fprintf(stderr, "wg_diag launch span %llu ticks\n", t1max - t0min);
+    fprintf(stderr, "wg_diag launch span %llu ticks of 100 MHz\n", t1max - t0min);
     return GOL_OK;
 }
 
@@ -797,7 +855,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
         if (k > 1) {
             a.blocked = nullptr;
             a.counts = nullptr;
-            a.band = c->band_multi;
+            a.band = band_for_depth(c, k);
             if (c->multi_variant == golk::kMultiWgDiag && !split) {
                 if (int rc = wg_diag_launch(c, a, k)) return rc;
             } else if (split && in_lo < in_hi) {

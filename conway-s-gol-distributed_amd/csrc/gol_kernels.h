@@ -57,6 +57,13 @@ enum : int {
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 
+// the k_step_wg variants (one band pipeline per workgroup)
+constexpr bool is_wg_variant(int v)
+{
+    return v == kMultiWg || v == kMultiWgHx || v == kMultiWgPg || v == kMultiWgNoBar ||
+           v == kMultiWgDiag;
+}
+
 // fast-path stencil variants (A/B-able in one process; kVariantDefault is shipped)
 enum : int {
     kVariantWindow = 0,     // k_step_fast: 3-row window, 1 row in flight
@@ -75,30 +82,41 @@ bool fast_path_ok(int width);
 // K turns per launch (temporal blocking): outputs rows [row_lo, row_hi) after `turns`
 // turns, reading rows [row_lo - turns, row_hi + turns) (mod modrows).  No blocked mask,
 // no counts.  turns in 2 .. multi_max_turns(variant).
-constexpr int kMaxTurnsPerLaunch = 16;
-int multi_max_turns(int variant);       // 16 for kMultiWg, 8 for the k_step_skew variants
+constexpr int kMaxTurnsPerLaunch = 32;
+// 32 for the helix k_step_wg variants, 16 for band-tiled k_step_wg, 8..12 for k_step_skew
+int multi_max_turns(int variant);
+// k_step_wg on helix tiles: wavefronts per workgroup at depth `turns` -- 4 up to K = 16, then
+// one more per 4 stages (K = 17..32: 5..8 waves of at most 4 stages, <= 72 VGPRs each)
+constexpr int wg_waves(int turns) { return turns <= 16 ? 4 : (turns + 3) / 4; }
+constexpr int kWgDeepMax = 32;
 // band height of the boundary launches of an overlapped step (rows next to the halos)
 constexpr int kOverlapBand = 16;
 // kMultiWgPg: stages per tile in the flag array, smallest band; it runs at depths K = 4, 8,
-// 12, 16 (every wave the same stage count) with band = 3K/4 - 5 (mod 6) (its steady loop
+// 12, 16 (every wave the same stage count) with band = 3K/4 - 5 (mod kWgU) (its steady loop
 // then ends on a whole unrolled iteration); other launches run as kMultiWgHx
 constexpr int kPgStages = 16;
 constexpr int kPgMinBand = 32;
+// k_step_wg's steady-loop unroll (its LDS ring slots are immediates) and wave 0's input rows
+// in flight (LDS-DMA ring of kWgDmaRows + 1 slots; kWgU a multiple of 3, of that and of 6).
+// 11 rows in flight (unroll 12) measured no faster than 5 at 65536^2, K = 4..16 (the launch
+// is not bound by the head's DMA latency) and cost PG 8-11 VGPRs: 5 / 6 stay.
+constexpr int kWgDmaRows = 5;
+constexpr int kWgU = 6;
 constexpr bool pg_ok(int turns, int band)
 {
     return turns % 4 == 0 && turns <= kPgStages && band >= kPgMinBand &&
-           (band + 5 - 3 * turns / 4) % 6 == 0;
+           (band + 5 - 3 * turns / 4) % kWgU == 0;
 }
 // the nearest band >= `band` kMultiWgPg runs at depth `turns` (0: none)
 constexpr int pg_band(int turns, int band)
 {
-    for (int b = band < kPgMinBand ? kPgMinBand : band; b < band + 6 + kPgMinBand; ++b)
+    for (int b = band < kPgMinBand ? kPgMinBand : band; b < band + kWgU + kPgMinBand; ++b)
         if (pg_ok(turns, b)) return b;
     return 0;
 }
 bool multi_ok(int width, int turns, int variant);
-// waves sharing one band pipeline (4 for kMultiWg, else 1)
-int multi_waves_per_band(int variant);
+// waves sharing one band pipeline at depth `turns` (k_step_wg: wg_waves, else 1)
+int multi_waves_per_band(int variant, int turns);
 // band pipelines per thread block (k_step_skew: 4 single-wave pipelines; k_step_wg: 1)
 int multi_pipes_per_block(int variant);
 bool multi_fits(int nw, int pitch, int rows);   // buffer < 2 GiB (k_step_skew buffer ranges)

@@ -618,10 +618,14 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
 
 int multi_max_turns(int variant)
 {
+    if (variant == kMultiWgHx || variant == kMultiWgPg) return kWgDeepMax;
     return is_wg_variant(variant) ? 16 : variant == kMultiSkewILW16 ? 12 : 8;
 }
 
-int multi_waves_per_band(int variant) { return is_wg_variant(variant) ? 4 : 1; }
+int multi_waves_per_band(int variant, int turns)
+{
+    return is_wg_variant(variant) ? wg_waves(turns) : 1;
+}
 
 int multi_pipes_per_block(int variant) { return is_wg_variant(variant) ? 1 : 4; }
 
@@ -687,7 +691,7 @@ static hipError_t launch_wg(const StepArgs &a0, int turns, hipStream_t s)
     const int ntx = hx ? (int)blocks : (int)multi_tiles(a.width, 2);
     void *fn = wg_kernel(turns, a.multi_variant);
     if (!fn) return hipErrorInvalidValue;
-    const int threads = 64 * multi_waves_per_band(a.multi_variant);
+    const int threads = 64 * multi_waves_per_band(a.multi_variant, turns);
     StepArgs args = a;
     const uint64_t *in = a.in;
     uint64_t *out = a.out;
@@ -729,7 +733,7 @@ static int multi_blocks_per_cu_v(int turns, int variant)
                                       : skew_kernel(V, turns, variant);
     if (!fn) return 0;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn,
-                                                        64 * multi_waves_per_band(variant),
+                                                        64 * multi_waves_per_band(variant, turns),
                                                         0) == hipSuccess
                ? blocks
                : 0;

@@ -42,13 +42,16 @@ struct WgSplit {
 // U = lcm(3, kWgRQ, kWgR) = 6.  Runtime slot indices (to deepen the rings to 12 DMA rows
 // and 8 hand-off slots without a longer unroll) measured no faster and cost ~10 VGPRs
 // (K = 16: 86, i.e. 5 waves/SIMD instead of 6).
-constexpr int kWgPD = 5;                                // wave 0's rows in flight
+constexpr int kWgPD = kWgDmaRows;                       // wave 0's rows in flight
 constexpr int kWgRQ = kWgPD + 1;                        // its LDS-DMA ring slots
 constexpr int kWgR = 6;                                 // hand-off ring slots per boundary
 // A wait gives up after this many polls (~2^22 x 64 cycles, >0.1 s): a broken hand-off then
 // ends the launch with a wrong board (caught by the parity tests) instead of hanging the GPU.
 constexpr int kWgSpinLimit = 1 << 22;
-constexpr int kWgLag = 3;                               // SYNC 2: consumer's initial lag (rows)
+// SYNC 2: consumer's initial lag (rows).  Each wave boundary adds it to the pipeline fill;
+// 1 measured as fast as 3 or slightly faster (16384^2 K = 16: 3.25 vs 3.27-3.33 us/turn; the
+// 8-strip shape 5.62 vs 5.66-5.95; 65536^2 equal)
+constexpr int kWgLag = 1;
 
 template <int NW, bool PG = false>
 struct WgShared {
@@ -115,7 +118,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     constexpr int J = WgSplit<K, NW>::J(W);
     constexpr bool FIRST = W == 0, LAST = W == NW - 1;
     constexpr int RQ = kWgRQ, PD = kWgPD, R = kWgR;
-    constexpr int U = 6;                                 // lcm(3, RQ, R): slots are immediates
+    constexpr int U = kWgU;                              // lcm(3, RQ, R): slots are immediates
     static_assert(U % 3 == 0 && U % RQ == 0 && U % R == 0, "steady unroll");
     constexpr int S0_ = 3 * G - 3;                       // local prologue steps
     constexpr int EMIT0 = 3 * G - 1;                     // first local step the last stage emits
@@ -219,6 +222,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     uint32_t avail = 0;                                  // consumer: rows known to be written
     uint32_t room = R;                                   // producer: rows it may write
     constexpr bool DIAG = SYNC == 3;
+    const unsigned long long d_r0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long d_t0 = DIAG ? __builtin_amdgcn_s_memtime() : 0, d_fw = 0, d_ew = 0,
                        d_nf = 0, d_ne = 0, d_first = 0;
     // input row q of local step l == q (SM = l mod U): wave 0 from its DMA ring, the others
@@ -552,7 +556,9 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     if constexpr (FIRST) __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // DMAs landed
     if constexpr (DIAG) {
         if (lane == 0 && a.counts) {
-            unsigned long long *d = a.counts + ((size_t)blockIdx.x * NW + W) * 8;
+            unsigned long long *d = a.counts + ((size_t)blockIdx.x * NW + W) * 10;
+            d[8] = d_r0;                                 // 100 MHz clock: comparable across XCDs
+            d[9] = __builtin_amdgcn_s_memrealtime();
             d[0] = __builtin_amdgcn_s_memtime() - d_t0;
             d[1] = d_first;
             d[2] = d_fw;

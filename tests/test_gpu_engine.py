@@ -201,6 +201,31 @@ def test_temporal_blocking_workgroup(gol, oracle, monkeypatch, mv, tpl, w, h, ba
     assert np.array_equal(got, oracle.bit_run(want_mid, w, turns + 3))
 
 
+@pytest.mark.parametrize("mv", [9, 12])
+@pytest.mark.parametrize("tpl", [17, 18, 20, 21, 23, 24, 25, 28, 31, 32])
+@pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 40), (384, 3, 8, 35), (8320, 41, 7, 33),
+                                            (16384, 70, 64, 20), (2048, 300, 137, 37),
+                                            (1920, 333, 37, 64), (4096, 1000, 250, 70),
+                                            (256, 200, 23, 50), (8064, 130, 43, 40)])
+def test_temporal_blocking_deep(gol, oracle, monkeypatch, mv, tpl, w, h, band, turns):
+    """k_step_wg on helix tiles at depths 17..32: wg_waves(K) = 5..8 wavefronts per workgroup,
+    at most 4 stages each (mv 12 runs these depths as plain helix).  Bit-exact incl. bands
+    shorter than K, tiny tori, short last bands and the even split leaving shallower
+    launches (35 turns at K = 32: 18 + 17)."""
+    monkeypatch.setenv("GOL_MULTI_VARIANT", str(mv))
+    start = oracle.gen_random(tpl * 17 + w + h, w, h)
+    with _engine(gol, w, h, band_rows=band, turns_per_launch=tpl) as e:
+        assert e.info().turns_per_launch == tpl
+        e.load_packed(start)
+        e.step(turns)
+        mid = e.read_packed()
+        e.step(turns + 5)
+        got = e.read_packed()
+    want_mid = oracle.bit_run(start, w, turns)
+    assert np.array_equal(mid, want_mid)
+    assert np.array_equal(got, oracle.bit_run(want_mid, w, turns + 5))
+
+
 @pytest.mark.parametrize("mv", [8, 9, 12])
 @pytest.mark.parametrize("key", ["16384x16384_seed2_t10000", "65536x65536_seed3_t1000"])
 def test_large_board_digests_workgroup(gol, monkeypatch, mv, key):
@@ -284,7 +309,7 @@ def test_interleaved_raw_layout(gol, oracle, monkeypatch):
 
 @pytest.mark.parametrize("mv", [7, 8, 9, 12])
 @pytest.mark.parametrize("n,K,tpl", [(2, 8, 4), (3, 5, 4), (4, 6, 8), (1, 7, 3), (2, 20, 16),
-                                     (3, 16, 12)])
+                                     (3, 16, 12), (2, 40, 32), (3, 30, 24)])
 def test_temporal_blocking_strips(gol, oracle, monkeypatch, mv, n, K, tpl):
     """Strip engines use the multi-turn pass within each K-turn halo window (k_step_skew
     and k_step_wg)."""
