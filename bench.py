@@ -187,6 +187,7 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    plan = eng.last_launches()          # the last gol_step call's launches (N > 1: one window)
     info = eng.info()
     launches = info.launches - launches0
     if world > 1:
@@ -200,9 +201,30 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
     out = {"W": W, "H": H, "steps": steps, "wall": wall, "gpu_ms": gpu_ms,
            "launches": launches, "K": info.turns_per_launch, "rows_local": rows_local,
            "band": info.band_rows, "fast": bool(info.fast_path), "halo": info.halo,
-           "transport": transport, "overlap": overlap}
+           "transport": transport, "overlap": overlap, "plan": plan}
     eng.close()
     return out
+
+
+KERNELS = {7: "k_step_skew<K> (interleaved layout, one pipeline per wave)",
+           8: "k_step_wg<K> (pipeline split over a workgroup, band tiles)",
+           9: "k_step_wg<K> (pipeline split over a workgroup, helix tiles)",
+           12: "k_step_wg<K> (helix tiles, parallelogram bands)",
+           0: "k_step_ring<D=3> (one turn per launch)"}
+
+
+def plan_summary(plan):
+    """Run-length summary of the engine's launches, e.g. '2 x (10 turns, kernel 7, band 137)',
+    and the kernel id that ran the most turns."""
+    runs, turns = [], {}
+    for k, var, band in plan:
+        turns[var] = turns.get(var, 0) + k
+        if runs and runs[-1][1] == (k, var, band):
+            runs[-1][0] += 1
+        else:
+            runs.append([1, (k, var, band)])
+    text = ", ".join(f"{n} x ({k} turns, kernel {v}, band {b})" for n, (k, v, b) in runs)
+    return text, (max(turns, key=turns.get) if turns else 0)
 
 
 def parallelism(a, world, m):
@@ -258,7 +280,9 @@ def main():
         bytes_board = BYTES_PER_CELL_UPDATE * cells_local
         bytes_k1 = BYTES_PER_CELL_UPDATE * turns_per_launch * cells_local
         achieved = bytes_board / (launch_us * 1e-6) / 1e9
-        traffic, traffic_src = pmc_traffic(W, K)
+        plan_text, kvar = plan_summary(m["plan"])
+        kdepth = max((k for k, v, _ in m["plan"] if v == kvar), default=K)
+        traffic, traffic_src = pmc_traffic(W, kdepth)
         out = {
             "metric": METRIC,
             "value": round(gcups, 2),
@@ -278,7 +302,8 @@ def main():
                        "board": [W, H], "turns": a.steps,
                        "parallelism": parallelism(a, world, m),
                        "band_rows": m["band"], "fast_path": m["fast"],
-                       "temporal_blocking_k": K},
+                       "temporal_blocking_k": K,
+                       "launch_plan": plan_text},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "definition": f"algorithmic HBM bytes of one blocked launch: 0.25/k B "
@@ -287,8 +312,7 @@ def main():
                                        f"{turns_per_launch:g} turns per launch on average, per "
                                        f"average launch time",
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": f"k_step_skew<K={K}> (interleaved layout)" if K > 1
-                                   else "k_step_ring<D=3>",
+                         "kernel": KERNELS.get(kvar, f"kernel {kvar}").replace("<K>", f"<K={kdepth}>"),
                          "launch_us": round(launch_us, 2), "launches": m["launches"],
                          "turns_per_launch": round(turns_per_launch, 3),
                          "bytes_per_launch": int(bytes_board)},
@@ -320,6 +344,7 @@ def main():
                 "ms_per_step": round(c3["wall"] * 1e3 / c3["steps"], 5),
                 "parallelism": parallelism(a, world, c3),
                 "band_rows": c3["band"], "temporal_blocking_k": c3["K"],
+                "launch_plan": plan_summary(c3["plan"])[0][:300],
                 "launch_us": round(l3, 2), "launches": c3["launches"],
                 "roofline_frac": round(b3 / (l3 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "valu_roofline_frac": round(g3 / world / VALU_PEAK_GCUPS, 4)}]

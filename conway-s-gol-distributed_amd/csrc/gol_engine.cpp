@@ -40,6 +40,13 @@ constexpr size_t kStagingBytes = 256u << 20;  // byte staging chunk for load / r
 
 }  // namespace
 
+// one temporal-blocking launch: depth, kernel (golk::kMulti*), band
+struct Launch {
+    int k = 0, var = 0, band = 0;
+};
+constexpr int kPlanMax = 128;               // launch plans cover gol_step / halo windows up to this
+constexpr size_t kLastCap = 4096;           // gol_last_launches records at most this many
+
 struct gol_ctx {
     gol_config cfg{};
     int device = 0;
@@ -52,6 +59,11 @@ struct gol_ctx {
     int multi_variant = golk::kMultiSkewILW16;  // temporal-blocking kernel (kMulti*)
     int band_multi = 64;                     // band height of the multi-turn kernel (depth tpl)
     int band_at[golk::kMaxTurnsPerLaunch + 1] = {};   // band_for_depth cache (0 = not yet)
+    // launch planner (autotuned engines): plan[t] = the first launch of the fastest measured
+    // sequence of launches for t turns (t <= kPlanMax; k = 0: no plan, use the even split)
+    std::vector<Launch> plan;
+    std::vector<Launch> last;                // launches of the last gol_step (gol_last_launches)
+    long long last_n = 0;
     int ncu = 0;                             // compute units of the device
     float tuned_us_per_turn = 0.f;           // autotune's best measurement (0 = not tuned)
     uint64_t *board[2] = {nullptr, nullptr};
@@ -165,57 +177,77 @@ int ensure_layout(gol_ctx *c, bool il)
     return GOL_OK;
 }
 
-// Turns fused into the next launch when `room` turns remain before the next sync point
-// (end of the gol_step call, or the next halo exchange of a strip engine).  The turns are
-// spread over ceil(room / tpl) launches of near-equal depth: a short tail launch costs
-// almost as much as a full one (K=2: 29 us vs K=6: 37 us on an 8448-row strip), so 128
-// turns at tpl 6 run as 18 x 6 + 4 x 5, not 21 x 6 + 2.  1 = the one-turn kernel.
-// gol_step and gol_halo_buffers both use this rule (the zero-copy halo layout must be
-// the layout the first launch after an exchange runs on).
-int launch_depth(const gol_ctx *c, int64_t room)
+// The band a kernel tuned at (K0, band0) runs at depth k.  A launch of another depth -- the
+// even split's shallower launches, a short gol_step, the last block before a halo exchange,
+// a planned launch -- runs a kernel with another residency (k_step_wg: 4..8 waves per
+// workgroup at 7 or 8 waves per SIMD; k_step_skew: 2..4 waves per SIMD), where band0 would
+// leave resident slots idle or spill a few pipelines into one more round (65536^2: K = 16's
+// band 607 fills 1791 of 1792 slots; a K = 20 launch has 1280).  Keep the tuned number of
+// rounds instead: the smallest band whose grid fits them at depth k (kMultiWgPg: the next
+// band it runs at).
+int band_same_rounds(const gol_ctx *c, int var, int K0, int band0, int k)
 {
-    if (c->tpl <= 1 || room < 2 || (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) ||
-        c->blocked_pending)
-        return 1;
-    const int64_t nl = (room + c->tpl - 1) / c->tpl;
-    const int k = (int)((room + nl - 1) / nl);
-    return golk::multi_ok(c->cfg.width, k, c->multi_variant) ? k : 1;
+    if (k == K0 || k < 2 || k > golk::kMaxTurnsPerLaunch) return band0;
+    const int lane_dw = golk::multi_lane_dwords(c->multi_words, var);
+    const int per = golk::multi_pipes_per_block(var);
+    const long long cap_t = (long long)c->ncu * golk::multi_blocks_per_cu(K0, c->multi_words, var) * per;
+    const long long cap_k = (long long)c->ncu * golk::multi_blocks_per_cu(k, c->multi_words, var) * per;
+    if (cap_t <= 0 || cap_k <= 0) return band0;
+    const int W = c->cfg.width, rows = c->buf_rows;
+    const long long pipes = golk::multi_pipes(W, rows, band0, lane_dw, var);
+    const long long rounds = std::max(1ll, (pipes + cap_t - 1) / cap_t);
+    int b = band0;
+    for (int band = 16; band <= std::max(rows, 16); ++band)
+        if (golk::multi_pipes(W, rows, band, lane_dw, var) <= rounds * cap_k) {
+            b = band;
+            break;
+        }
+    if (var == golk::kMultiWgPg && golk::pg_ok(k, golk::pg_band(k, b))) b = golk::pg_band(k, b);
+    return b;
 }
 
-// Band height of a launch of depth k.  band_multi was chosen (tuned) for depth tpl; a
-// launch of another depth -- the even split's shallower launches, a short gol_step, the last
-// block before a halo exchange -- runs a kernel with another residency (k_step_wg: 4..8 waves
-// per workgroup at 7 or 8 waves per SIMD; k_step_skew: 2..4 waves per SIMD), where that band
-// would leave resident slots idle or spill a few pipelines into one more round (65536^2:
-// K = 16's band 607 fills 1791 of 1792 slots; a K = 20 launch has 1280).  Keep the tuned
-// number of rounds instead: the smallest band whose grid fits them at depth k (kMultiWgPg:
-// the next band it runs at).  A band the caller fixed (gol_config.band_rows) is kept.
+// band_same_rounds for the engine's kernel and depth (cached); a band the caller fixed
+// (gol_config.band_rows) is kept
 int band_for_depth(gol_ctx *c, int k)
 {
     if (k == c->tpl || c->cfg.band_rows > 0 || k < 2 || k > golk::kMaxTurnsPerLaunch)
         return c->band_multi;
     int &b = c->band_at[k];
-    if (b > 0) return b;
-    b = c->band_multi;
-    const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
-    const int per = golk::multi_pipes_per_block(c->multi_variant);
-    const long long cap_t =
-        (long long)c->ncu * golk::multi_blocks_per_cu(c->tpl, c->multi_words, c->multi_variant) * per;
-    const long long cap_k =
-        (long long)c->ncu * golk::multi_blocks_per_cu(k, c->multi_words, c->multi_variant) * per;
-    if (cap_t <= 0 || cap_k <= 0) return b;
-    const int W = c->cfg.width, rows = c->buf_rows;
-    const long long pipes = golk::multi_pipes(W, rows, c->band_multi, lane_dw, c->multi_variant);
-    const long long rounds = std::max(1ll, (pipes + cap_t - 1) / cap_t);
-    for (int band = 16; band <= std::max(rows, 16); ++band)
-        if (golk::multi_pipes(W, rows, band, lane_dw, c->multi_variant) <= rounds * cap_k) {
-            b = band;
-            break;
-        }
-    if (c->multi_variant == golk::kMultiWgPg && golk::pg_ok(k, golk::pg_band(k, b)))
-        b = golk::pg_band(k, b);
+    if (b <= 0) b = band_same_rounds(c, c->multi_variant, c->tpl, c->band_multi, k);
     return b;
 }
+
+// The next launch when `room` turns remain before the next sync point (end of the gol_step
+// call, or the next halo exchange of a strip engine).  k = 1: the one-turn kernel.
+//  * Autotuned engines follow the launch plan for room <= kPlanMax: the sequence of launches
+//    (depth and kernel) the create-time timing table says is fastest.  A short launch costs
+//    nearly as much as a full one and the kernels differ in that fixed cost (65536^2,
+//    profiles/r02_launch_table_65536.log: k_step_skew 260 us at K = 6 and 384 at K = 10;
+//    k_step_wg 413 us at K = 4, 459 at 12, 595 at 16), so 20 turns run best as 10 + 10 on
+//    k_step_skew although k_step_wg at K = 16 is the fastest per turn.  Longer stretches run
+//    full launches of the tuned kernel and depth first.
+//  * Otherwise the turns are spread over ceil(room / tpl) launches of near-equal depth: 128
+//    turns at tpl 6 run as 18 x 6 + 4 x 5, not 21 x 6 + 2.
+// gol_step and gol_halo_buffers both use this rule (the zero-copy halo layout must be the
+// layout the first launch after an exchange runs on; every planned kernel runs on the
+// interleaved layout).
+Launch plan_launch(gol_ctx *c, int64_t room)
+{
+    Launch L{1, c->multi_variant, c->band};
+    if (c->tpl <= 1 || room < 2 || (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) ||
+        c->blocked_pending)
+        return L;
+    if (!c->plan.empty()) {
+        if (room > kPlanMax) return Launch{c->tpl, c->multi_variant, c->band_multi};
+        if (c->plan[room].k >= 2) return c->plan[room];
+    }
+    const int64_t nl = (room + c->tpl - 1) / c->tpl;
+    const int k = (int)((room + nl - 1) / nl);
+    if (!golk::multi_ok(c->cfg.width, k, c->multi_variant)) return L;
+    return Launch{k, c->multi_variant, band_for_depth(c, k)};
+}
+
+int launch_depth(gol_ctx *c, int64_t room) { return plan_launch(c, room).k; }
 
 // the word layout a launch of depth k runs on
 bool stepping_il(const gol_ctx *c, int k)
@@ -407,6 +439,69 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
         }
     }
     if (pick_t > 0.f) best = pick_t;
+    // Launch planner (tune_k and tune_variant only: nothing pinned).  For each kernel, its
+    // fastest (K, band) is a family; time one launch of every family at every depth 2..16
+    // (band_same_rounds), then plan, for every t <= kPlanMax turns, the sequence of launches
+    // with the least total measured time (plan_launch).  All candidates run on the
+    // interleaved layout, so launches of different kernels mix freely.
+    std::vector<Launch> plan;
+    if (tune_k && tune_variant && pick_t > 0.f) {
+        struct Fam {
+            int var, K, band;
+            float T[golk::kMaxTurnsPerLaunch + 1];
+            int band_k[golk::kMaxTurnsPerLaunch + 1];
+        };
+        std::vector<Fam> fams;
+        for (int var : vars) {
+            int bi = -1;
+            for (size_t i = 0; i < cand.size(); ++i)
+                if (cand[i].var == var && t[i] > 0.f && (bi < 0 || t[i] < t[bi])) bi = (int)i;
+            if (bi < 0 || !golk::multi_is_il(c->multi_words, var)) continue;
+            Fam f{var, cand[bi].K, cand[bi].band, {}, {}};
+            for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k) {
+                f.T[k] = 0.f;
+                f.band_k[k] = 0;
+                // (k_step_wg runs depths 2, 3 as k_step_skew: that family covers them)
+                if (k > 16 || !golk::multi_ok(c->cfg.width, k, var) ||
+                    (golk::is_wg_variant(var) && k < 4))
+                    continue;
+                f.band_k[k] = band_same_rounds(c, var, f.K, f.band, k);
+                for (int pass = 0; pass < 2; ++pass) {
+                    const float v = time_one(Cand{var, k, f.band_k[k]}, reps) * (float)k;
+                    if (v > 0.f && (f.T[k] == 0.f || v < f.T[k])) f.T[k] = v;
+                }
+            }
+            fams.push_back(f);
+        }
+        const float inf = 1e30f;
+        std::vector<float> cost(kPlanMax + 1, inf);
+        plan.assign(kPlanMax + 1, Launch{});
+        cost[0] = 0.f;
+        for (int r = 2; r <= kPlanMax; ++r)
+            for (const Fam &f : fams)
+                for (int k = 2; k <= std::min(r, golk::kMaxTurnsPerLaunch); ++k) {
+                    if (f.T[k] <= 0.f || r - k == 1 || cost[r - k] >= inf) continue;
+                    const float v = cost[r - k] + f.T[k];
+                    if (v < cost[r]) {
+                        cost[r] = v;
+                        plan[r] = Launch{k, f.var, f.band_k[k]};
+                    }
+                }
+        if (getenv("GOL_AUTOTUNE_LOG")) {
+            for (const Fam &f : fams)
+                for (int k = 2; k <= 16; ++k)
+                    if (f.T[k] > 0.f)
+                        fprintf(stderr, "autotune launch var=%d K=%d band=%d us=%.1f\n", f.var, k,
+                                f.band_k[k], f.T[k] * 1000.f);
+            for (int r : {8, 16, 20, 32, 64, 128})
+                if (r <= kPlanMax) {
+                    fprintf(stderr, "autotune plan %d turns: %.1f us =", r, cost[r] * 1000.f);
+                    for (int q = r; q >= 2 && plan[q].k >= 2; q -= plan[q].k)
+                        fprintf(stderr, " %d(var %d, band %d)", plan[q].k, plan[q].var, plan[q].band);
+                    fprintf(stderr, "\n");
+                }
+        }
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipGetLastError();
@@ -414,6 +509,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     c->tpl = pick.K;
     c->band_multi = pick.band;
     for (int &b : c->band_at) b = 0;
+    c->plan = std::move(plan);
     c->tuned_us_per_turn = best * 1000.f;
 }
 
@@ -806,6 +902,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
         }
     } ring;
     const bool ctl = c->control_used.load();
+    c->last.clear();
+    c->last_n = 0;
     for (int64_t t = 0; t < turns;) {
         if (ctl) {
             int w = c->control.load();
@@ -823,7 +921,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
         }
         int64_t room = turns - t;
         if (is_strip(c)) room = std::min<int64_t>(room, c->halo_valid);
-        const int k = launch_depth(c, room);
+        const Launch plan = plan_launch(c, room);
+        const int k = plan.k;
         // rows computed: torus -> all; strip -> [s, buf_rows - s) after turn s since exchange
         const int s0 = is_strip(c) ? c->cfg.halo - c->halo_valid : 0;
         if (is_strip(c)) {
@@ -855,7 +954,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
         if (k > 1) {
             a.blocked = nullptr;
             a.counts = nullptr;
-            a.band = band_for_depth(c, k);
+            a.band = plan.band;
+            a.multi_variant = plan.var;
             if (c->multi_variant == golk::kMultiWgDiag && !split) {
                 if (int rc = wg_diag_launch(c, a, k)) return rc;
             } else if (split && in_lo < in_hi) {
@@ -878,6 +978,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
                 HIP_OR_FAIL(c, golk::launch_step_multi(a, k, split ? c->side : c->stream));
             }
             a.band = c->band;
+            a.multi_variant = c->multi_variant;
         } else if (split) {
             // one-turn launches: interior now, the 2 x (halo) boundary rows after the receives
             a.blocked = c->blocked_pending ? c->blocked : nullptr;
@@ -921,6 +1022,9 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
         c->turn += k;
         c->progress.store(c->turn);
         c->launches += 1;
+        if (c->last.size() < kLastCap)
+            c->last.push_back(k > 1 ? Launch{k, plan.var, plan.band} : Launch{1, 0, c->band});
+        ++c->last_n;
         t += k;
         if (is_strip(c)) c->halo_valid -= k;
         if (c->blocked_pending) {
@@ -950,6 +1054,19 @@ int gol_step(gol_ctx *c, int64_t turns)
     if (!c || turns < 0) return GOL_EINVAL;
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     return step_impl(c, turns, nullptr);
+}
+
+int gol_last_launches(gol_ctx *c, int32_t *turns, int32_t *kernel, int32_t *band, int32_t cap)
+{
+    if (!c || cap < 0 || (cap > 0 && (!turns || !kernel || !band))) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    const int n = (int)std::min<size_t>((size_t)cap, c->last.size());
+    for (int i = 0; i < n; ++i) {
+        turns[i] = c->last[i].k;
+        kernel[i] = c->last[i].var;
+        band[i] = c->last[i].band;
+    }
+    return (int)std::min<long long>(c->last_n, 0x7fffffff);
 }
 
 int gol_step_overlap(gol_ctx *c, int64_t turns, void *recv_stream)

@@ -115,6 +115,9 @@ SIGNATURES = {
     "gol_step": (_i32, [_vp, _i64]),
     "gol_set_control": (_i32, [_vp, _i32]),
     "gol_get_progress": (_i32, [_vp, _i64p, ctypes.POINTER(ctypes.c_int32)]),
+    "gol_last_launches": (_i32, [_vp, ctypes.POINTER(ctypes.c_int32),
+                                 ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                 ctypes.c_int32]),
     "gol_stream_wait": (_i32, [_vp, _vp]),
     "gol_step_overlap": (_i32, [_vp, _i64, _vp]),
     "gol_snapshot": (_i32, [_vp, _i64p, _i64p]),

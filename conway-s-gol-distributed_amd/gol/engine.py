@@ -123,6 +123,12 @@ class Engine:
         self._c(self._L.gol_get_progress(self._h, ctypes.byref(t), ctypes.byref(p)))
         return int(t.value), bool(p.value)
 
+    def last_launches(self, cap: int = 4096):
+        """[(turns, kernel id, band rows)] of the launches the last step() ran."""
+        arrs = [(ctypes.c_int32 * cap)() for _ in range(3)]
+        n = self._c(self._L.gol_last_launches(self._h, *arrs, int(cap)))
+        return [(arrs[0][i], arrs[1][i], arrs[2][i]) for i in range(min(n, cap))]
+
     # -- overlapped halo exchange (gol_stream_wait / gol_step_overlap)
     def stream_wait(self, stream_ptr: int):
         """Make `stream_ptr` wait for the work queued on the engine so far."""

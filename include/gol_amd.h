@@ -144,6 +144,13 @@ int gol_step(gol_ctx *ctx, int64_t turns);
 #define GOL_CONTROL_PAUSE  1
 #define GOL_CONTROL_STOP   2
 int gol_set_control(gol_ctx *ctx, int32_t word);
+
+/* The launches the last gol_step / gol_step_overlap call ran (planner introspection for
+ * benchmarks and tests; no reference counterpart): up to `cap` entries of turns fused, kernel
+ * (the engine's temporal-blocking kernel id; turns == 1: the one-turn stencil, kernel 0) and
+ * band rows.  Returns the number of launches (may exceed cap; entries past 4096 are not
+ * recorded), or a negative GOL_E* code. */
+int gol_last_launches(gol_ctx *ctx, int32_t *turns, int32_t *kernel, int32_t *band, int32_t cap);
 /* Lock-free progress read for a controlling thread: *turn = turns enqueued so far (the
  * board reaches it at the next gol_sync), *parked = 1 while gol_step is parked on PAUSE
  * (the board is then complete at *turn).  Either pointer may be NULL. */

@@ -226,6 +226,27 @@ def test_temporal_blocking_deep(gol, oracle, monkeypatch, mv, tpl, w, h, band, t
     assert np.array_equal(got, oracle.bit_run(want_mid, w, turns + 5))
 
 
+def test_launch_planner(gol, oracle):
+    """Autotuned engines follow the create-time launch plan: short gol_step calls run the
+    measured-fastest mix of kernels and depths (kernels switch between launches on the shared
+    interleaved layout).  Bit-exact against the oracle across calls of 1, 2, 3, 5, 20 and 37
+    turns; every planned launch fuses >= 2 turns, and the launches add up to the call."""
+    w, h = 16384, 4096                               # 2^20 words: the autotune runs
+    start = oracle.gen_random(77, w, h)
+    board = start
+    with _engine(gol, w, h) as e:
+        e.load_packed(start)
+        for turns in (1, 2, 3, 5, 20, 37):
+            e.step(turns)
+            plan = e.last_launches()
+            assert sum(k for k, _, _ in plan) == turns
+            if turns >= 2:
+                assert all(k >= 2 for k, _, _ in plan), plan
+            assert all(b > 0 for _, _, b in plan)
+        got = e.read_packed()
+    assert np.array_equal(got, oracle.bit_run(board, w, 68))
+
+
 @pytest.mark.parametrize("mv", [8, 9, 12])
 @pytest.mark.parametrize("key", ["16384x16384_seed2_t10000", "65536x65536_seed3_t1000"])
 def test_large_board_digests_workgroup(gol, monkeypatch, mv, key):
