@@ -256,6 +256,12 @@ def main():
     # a dedicated (non-default) stream shared by the engine, the events and RCCL
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
+    # torch creates the HIP stream on first use (~8 ms on the GPU box): do that now, not
+    # between the engine's create-time autotune and the warm-up -- an idle MI355X lowers its
+    # clock, and the short timed region then runs before it has ramped back
+    # (profiles/r02_clock_pmc_bench20.txt, tools/phase_timing.py)
+    stream.synchronize()
+    _ = stream.cuda_stream
 
     m = measure(a, a.size, a.steps, a.warmup, world, rank, gpu, dev, dev_ids, stream)
     c3 = None
