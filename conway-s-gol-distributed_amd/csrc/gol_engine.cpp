@@ -413,11 +413,41 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
         const float us = time_one(cand.back(), 12) * 1000.f * cand.back().K;   // per launch
         if (us > 0.f) reps = std::max(3, std::min(24, (int)(1000.f / us) + 1));
     }
-    for (int pass = 0; pass < 2; ++pass)
-        for (size_t i = 0; i < cand.size(); ++i) {
-            const float v = time_one(cand[i], reps);
-            if (v > 0.f && (t[i] == 0.f || v < t[i])) t[i] = v;
+    auto measure = [&](size_t from) {
+        for (int pass = 0; pass < 2; ++pass)
+            for (size_t i = from; i < cand.size(); ++i) {
+                const float v = time_one(cand[i], reps);
+                if (v > 0.f && (t[i] == 0.f || v < t[i])) t[i] = v;
+            }
+    };
+    measure(0);
+    // refine: the bands next to each kernel's best (the coarse list steps by up to 50 %, and
+    // a one-round grid's fill changes with every band: 16384^2 parallelogram K = 16 ran
+    // 3.35 / 3.25 / 3.70 us per turn at bands 43 / 55 / 67)
+    {
+        const size_t n0 = cand.size();
+        for (int var : vars) {
+            int bi = -1;
+            for (size_t i = 0; i < n0; ++i)
+                if (cand[i].var == var && t[i] > 0.f && (bi < 0 || t[i] < t[bi])) bi = (int)i;
+            if (bi < 0) continue;
+            const Cand b = cand[bi];
+            const int step = var == golk::kMultiWgPg ? golk::kWgU : std::max(2, b.band / 16);
+            for (int d : {-2, -1, 1, 2}) {
+                int band = b.band + d * step;
+                if (var == golk::kMultiWgPg) band = golk::pg_band(b.K, band);
+                if (band < 16 || band > std::max(c->cfg.rows, 16)) continue;
+                bool seen = false;
+                for (const Cand &x : cand)
+                    seen |= x.var == var && x.K == b.K && x.band == band;
+                if (!seen) {
+                    cand.push_back({var, b.K, band});
+                    t.push_back(0.f);
+                }
+            }
         }
+        measure(n0);
+    }
     float best = 0.f;
     for (size_t i = 0; i < cand.size(); ++i)
         if (t[i] > 0.f && (best == 0.f || t[i] < best)) best = t[i];
