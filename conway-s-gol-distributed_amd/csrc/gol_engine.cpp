@@ -421,16 +421,20 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             }
     };
     measure(0);
-    // refine: the bands next to each kernel's best (the coarse list steps by up to 50 %, and
-    // a one-round grid's fill changes with every band: 16384^2 parallelogram K = 16 ran
-    // 3.35 / 3.25 / 3.70 us per turn at bands 43 / 55 / 67)
+    // refine: the bands next to the best of each (kernel, K) (the coarse list steps by up to
+    // 50 %, and a one-round grid's fill changes with every band: 16384^2 parallelogram K = 16
+    // ran 3.35 / 3.25 / 3.70 us per turn at bands 43 / 55 / 67)
     {
         const size_t n0 = cand.size();
-        for (int var : vars) {
+        for (size_t j = 0; j < n0; ++j) {
+            // the best band of each (kernel, K)
+            const int var = cand[j].var;
             int bi = -1;
             for (size_t i = 0; i < n0; ++i)
-                if (cand[i].var == var && t[i] > 0.f && (bi < 0 || t[i] < t[bi])) bi = (int)i;
-            if (bi < 0) continue;
+                if (cand[i].var == var && cand[i].K == cand[j].K && t[i] > 0.f &&
+                    (bi < 0 || t[i] < t[bi]))
+                    bi = (int)i;
+            if (bi != (int)j) continue;
             const Cand b = cand[bi];
             const int step = var == golk::kMultiWgPg ? golk::kWgU : std::max(2, b.band / 16);
             for (int d : {-2, -1, 1, 2}) {
