@@ -94,11 +94,12 @@ def pmc_traffic(size, k):
     tools/profile.sh + tools/summarize_profile.py), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_k{k}_{size}_summary.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    return d.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    for path in reversed(files):                 # the newest pass that holds PMC bytes
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("traffic_bytes_per_launch"):
+            return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_share():
@@ -351,6 +352,8 @@ def main():
                 "parallelism": parallelism(a, world, c3),
                 "band_rows": c3["band"], "temporal_blocking_k": c3["K"],
                 "launch_plan": plan_summary(c3["plan"])[0][:300],
+                "traffic": pmc_traffic(c3["W"], c3["K"])[0],
+                "traffic_source": pmc_traffic(c3["W"], c3["K"])[1],
                 "launch_us": round(l3, 2), "launches": c3["launches"],
                 "roofline_frac": round(b3 / (l3 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "valu_roofline_frac": round(g3 / world / VALU_PEAK_GCUPS, 4)}]
