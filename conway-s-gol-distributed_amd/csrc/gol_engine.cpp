@@ -56,6 +56,7 @@ struct gol_ctx {
     int variant = golk::kVariantDefault;
     int tpl = 1;                             // turns per stencil launch (temporal blocking)
     int multi_words = 2;                     // k_step_multi words per lane
+    unsigned wg_prio = 0;                    // k_step_wg priority override (GOL_WG_PRIO, tools)
     int multi_variant = golk::kMultiSkewILW16;  // temporal-blocking kernel (kMulti*)
     int band_multi = 64;                     // band height of the multi-turn kernel (depth tpl)
     int band_at[golk::kMaxTurnsPerLaunch + 1] = {};   // band_for_depth cache (0 = not yet)
@@ -380,6 +381,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     a.cnt_hi = 0;
     a.variant = c->variant;
     a.multi_words = c->multi_words;
+    a.wg_prio = c->wg_prio;
     if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
                                  c->buf_rows, 12345, c->stream) != hipSuccess)
         return;
@@ -617,6 +619,11 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     // 87 VGPRs at K=4), K = 6 on large boards (64-row bands), K = 4 on smaller ones
     c->multi_words = 1;
     if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
+    if (const char *v = getenv("GOL_WG_PRIO")) {          // A/B experiments only: "3210" =
+        for (int w = 0; w < 4 && v[w] >= '0' && v[w] <= '3'; ++w)   // wave 0..3's priority
+            c->wg_prio |= (unsigned)(v[w] - '0') << (2 * w);
+        if (!c->wg_prio) c->wg_prio = 0x100;              // all zero: still an override
+    }
     if (const char *v = getenv("GOL_MULTI_VARIANT")) {    // A/B experiments only
         const int k = atoi(v);
         c->multi_variant = (k >= 0 && k < golk::kMultiCount) || k > golk::kMultiAblate
@@ -924,6 +931,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
     a.band = c->band;
     a.variant = c->variant;
     a.multi_words = c->multi_words;
+    a.wg_prio = c->wg_prio;
     a.multi_variant = c->multi_variant;
     // control word: with a controlling thread present, keep at most kCtlDepth launches
     // queued so a pause / stop takes effect within that many launches

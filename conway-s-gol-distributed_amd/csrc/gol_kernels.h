@@ -31,6 +31,9 @@ struct StepArgs {
     unsigned *xflags;                  // per (tile, stage): epoch of its last publication
     unsigned xlanes;                   // virtual lanes per published row
     unsigned epoch;                    // this launch's epoch (above every earlier launch's)
+    // k_step_wg wave priorities (4-wave workgroups): wave w runs at s_setprio
+    // (wg_prio >> 2w) & 3; 0 = the built-in grading
+    unsigned wg_prio;
 };
 
 // temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkewILW16 is shipped)

@@ -218,7 +218,16 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     // priorities graded down the chain: upstream waves outrank their consumers (equal
     // priorities left the followers waiting for the head's rows at ~93 % of their steps,
     // tools/wg_diag.py; graded: 65536^2 K=16 44.6 -> 38.2 us/turn)
-    if constexpr (SYNC >= 2) __builtin_amdgcn_s_setprio((NW - 1 - W) * 3 / (NW - 1));
+    if constexpr (SYNC >= 2) {
+        const unsigned pr = NW == 4 && a.wg_prio ? (a.wg_prio >> (2 * W)) & 3u
+                                                 : (unsigned)((NW - 1 - W) * 3 / (NW - 1));
+        switch (pr) {                                    // (s_setprio takes an immediate)
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+        }
+    }
     uint32_t avail = 0;                                  // consumer: rows known to be written
     uint32_t room = R;                                   // producer: rows it may write
     constexpr bool DIAG = SYNC == 3;

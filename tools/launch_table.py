@@ -22,13 +22,14 @@ def main():
     ap.add_argument("--mv", default="7,9,12")
     ap.add_argument("--k", default="4,6,8,10,12,16,20")
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--band", type=int, default=0, help="fixed band rows (0: autotuned per k)")
     a = ap.parse_args()
     W = H = a.size
     stream = torch.cuda.Stream()
     for mv in a.mv.split(","):
         os.environ["GOL_MULTI_VARIANT"] = mv
         for k in [int(x) for x in a.k.split(",")]:
-            e = gol.Engine(W, H, device=0, turns_per_launch=k)
+            e = gol.Engine(W, H, device=0, turns_per_launch=k, band_rows=a.band)
             inf = e.info()
             if inf.turns_per_launch != k:
                 e.close()
