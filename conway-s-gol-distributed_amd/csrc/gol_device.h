@@ -222,6 +222,7 @@ constexpr bool is_il_variant(int v)
 void *skew_kernel(int words_per_lane, int turns, int variant);   // gol_skew.hip
 void *wg_kernel(int turns, int variant);                          // gol_wg.hip
 void *wg_hx_kernel(int turns, bool pg);                           // gol_wg_hx.hip
+void *wg_ser_kernel(int turns, bool pg);                          // gol_wg_ser.hip
 void *wg_deep_kernel_a(int turns);                                // gol_wg_deep_a.hip (17..24)
 void *wg_deep_kernel_b(int turns);                                // gol_wg_deep_b.hip (25..32)
 

@@ -203,7 +203,9 @@ int band_same_rounds(const gol_ctx *c, int var, int K0, int band0, int k)
             b = band;
             break;
         }
-    if (var == golk::kMultiWgPg && golk::pg_ok(k, golk::pg_band(k, b))) b = golk::pg_band(k, b);
+    const bool ser = var == golk::kMultiWgPgS;
+    if (golk::is_pg_variant(var) && golk::pg_ok(k, golk::pg_band(k, b, ser), ser))
+        b = golk::pg_band(k, b, ser);
     return b;
 }
 
@@ -279,7 +281,9 @@ static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
 {
     a.xrows = nullptr;
     a.xflags = nullptr;
-    if (a.multi_variant != golk::kMultiWgPg || !golk::pg_ok(k, a.band)) return hipSuccess;
+    if (!golk::is_pg_variant(a.multi_variant) ||
+        !golk::pg_ok(k, a.band, a.multi_variant == golk::kMultiWgPgS))
+        return hipSuccess;
     const long long T =
         golk::multi_pipes(a.width, a.row_hi - a.row_lo, a.band, 2, a.multi_variant);
     const size_t lanes = (size_t)T * 62 + 64;
@@ -326,7 +330,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     if (words < (1ll << 20)) return;                 // < 64 Mi cells: keep the defaults
     std::vector<int> vars{c->multi_variant};
     if (tune_variant)
-        vars = {golk::kMultiSkewILW16, golk::kMultiWg, golk::kMultiWgHx, golk::kMultiWgPg};
+        vars = {golk::kMultiSkewILW16, golk::kMultiWg, golk::kMultiWgHx, golk::kMultiWgPg,
+                golk::kMultiWgHxS, golk::kMultiWgPgS};
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     struct Cand {
@@ -357,8 +362,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                         break;
                     }
             }
-            if (var == golk::kMultiWgPg) {   // the nearest bands it runs at (golk::pg_ok)
-                for (int &b : bands) b = golk::pg_band(K, b);
+            if (golk::is_pg_variant(var)) {   // the nearest bands it runs at (golk::pg_ok)
+                for (int &b : bands) b = golk::pg_band(K, b, var == golk::kMultiWgPgS);
                 bands.erase(std::remove(bands.begin(), bands.end(), 0), bands.end());
             }
             std::sort(bands.begin(), bands.end());
@@ -438,10 +443,11 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                     bi = (int)i;
             if (bi != (int)j) continue;
             const Cand b = cand[bi];
-            const int step = var == golk::kMultiWgPg ? golk::kWgU : std::max(2, b.band / 16);
+            const int step = golk::is_pg_variant(var) ? golk::kWgU : std::max(2, b.band / 16);
             for (int d : {-2, -1, 1, 2}) {
                 int band = b.band + d * step;
-                if (var == golk::kMultiWgPg) band = golk::pg_band(b.K, band);
+                if (golk::is_pg_variant(var))
+                    band = golk::pg_band(b.K, band, var == golk::kMultiWgPgS);
                 if (band < 16 || band > std::max(c->cfg.rows, 16)) continue;
                 bool seen = false;
                 for (const Cand &x : cand)
@@ -1004,6 +1010,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
                 golk::StepArgs b = a;
                 // concurrent launches cannot share the published-row scratch
                 if (b.multi_variant == golk::kMultiWgPg) b.multi_variant = golk::kMultiWgHx;
+                if (b.multi_variant == golk::kMultiWgPgS) b.multi_variant = golk::kMultiWgHxS;
                 b.row_lo = in_lo;
                 b.row_hi = in_hi;
                 HIP_OR_FAIL(c, golk::launch_step_multi(b, k, c->stream));

@@ -56,7 +56,10 @@ enum : int {
     kMultiWgPg = 12,        // kMultiWgHx with parallelogram bands: a band's stages take their
                             //   last 2 input rows from the band below (published through
                             //   memory) instead of recomputing a 2K-row halo (band >= kPgMinBand)
-    kMultiCount = 13,
+    kMultiWgHxS = 13,       // kMultiWgHx with each wave's stages in order within a step (fill
+                            //   and drain of 2 instead of 3 steps per stage)
+    kMultiWgPgS = 14,       // kMultiWgPg, stages in order (band rule: golk::pg_ok(.., true))
+    kMultiCount = 15,
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 
@@ -64,7 +67,7 @@ enum : int {
 constexpr bool is_wg_variant(int v)
 {
     return v == kMultiWg || v == kMultiWgHx || v == kMultiWgPg || v == kMultiWgNoBar ||
-           v == kMultiWgDiag;
+           v == kMultiWgDiag || v == kMultiWgHxS || v == kMultiWgPgS;
 }
 
 // fast-path stencil variants (A/B-able in one process; kVariantDefault is shipped)
@@ -105,17 +108,23 @@ constexpr int kPgMinBand = 32;
 // is not bound by the head's DMA latency) and cost PG 8-11 VGPRs: 5 / 6 stay.
 constexpr int kWgDmaRows = 5;
 constexpr int kWgU = 6;
-constexpr bool pg_ok(int turns, int band)
+// (ser: kMultiWgPgS, prologue 2G - 2 steps instead of 3G - 3, G = turns / 4)
+constexpr bool pg_ok(int turns, int band, bool ser = false)
 {
     return turns % 4 == 0 && turns <= kPgStages && band >= kPgMinBand &&
-           (band + 5 - 3 * turns / 4) % kWgU == 0;
+           (band + 2 - (ser ? 2 : 3) * (turns / 4 - 1)) % kWgU == 0;
 }
-// the nearest band >= `band` kMultiWgPg runs at depth `turns` (0: none)
-constexpr int pg_band(int turns, int band)
+// the nearest band >= `band` kMultiWgPg / kMultiWgPgS runs at depth `turns` (0: none)
+constexpr int pg_band(int turns, int band, bool ser = false)
 {
     for (int b = band < kPgMinBand ? kPgMinBand : band; b < band + kWgU + kPgMinBand; ++b)
-        if (pg_ok(turns, b)) return b;
+        if (pg_ok(turns, b, ser)) return b;
     return 0;
+}
+constexpr bool is_pg_variant(int v) { return v == kMultiWgPg || v == kMultiWgPgS; }
+constexpr bool is_helix_variant(int v)
+{
+    return v == kMultiWgHx || v == kMultiWgPg || v == kMultiWgHxS || v == kMultiWgPgS;
 }
 bool multi_ok(int width, int turns, int variant);
 // waves sharing one band pipeline at depth `turns` (k_step_wg: wg_waves, else 1)

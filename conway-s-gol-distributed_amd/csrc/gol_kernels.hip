@@ -619,6 +619,7 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
 int multi_max_turns(int variant)
 {
     if (variant == kMultiWgHx || variant == kMultiWgPg) return kWgDeepMax;
+    if (variant == kMultiWgHxS || variant == kMultiWgPgS) return 16;
     return is_wg_variant(variant) ? 16 : variant == kMultiSkewILW16 ? 12 : 8;
 }
 
@@ -648,7 +649,7 @@ long long multi_tiles(int width, int lane_dwords)
 long long multi_pipes(int width, int rows, int band, int lane_dwords, int variant)
 {
     const long long nb = (rows + band - 1) / band;
-    if (variant == kMultiWgHx || variant == kMultiWgPg) {
+    if (is_helix_variant(variant)) {
         // stored virtual lanes run up to nb (nw + 4) - 3; tile t stores [62t + 1, 62t + 62]
         const long long nwv = (width + 63) / 64 + 4;
         return (nb * nwv - 3 + 61) / 62;
@@ -682,9 +683,11 @@ bool multi_fits(int nw, int pitch, int rows)
 static hipError_t launch_wg(const StepArgs &a0, int turns, hipStream_t s)
 {
     StepArgs a = a0;                                    // other shapes / no scratch: helix
-    if (a.multi_variant == kMultiWgPg && (!pg_ok(turns, a.band) || !a.xrows || !a.xflags))
-        a.multi_variant = kMultiWgHx;
-    const bool hx = a.multi_variant == kMultiWgHx || a.multi_variant == kMultiWgPg;
+    const bool ser = a.multi_variant == kMultiWgPgS;
+    if (is_pg_variant(a.multi_variant) &&
+        (!pg_ok(turns, a.band, ser) || !a.xrows || !a.xflags))
+        a.multi_variant = ser ? kMultiWgHxS : kMultiWgHx;
+    const bool hx = is_helix_variant(a.multi_variant);
     const long long blocks =
         multi_pipes(a.width, a.row_hi - a.row_lo, a.band, 2, a.multi_variant);
     // band tiling: tiles per band; helix: the tile count itself (blockIdx.x = tile)

@@ -108,7 +108,7 @@ __device__ __forceinline__ void lds_store_counter(uint32_t *p, uint32_t v)
 // trapezoid: it breaks the torus cycle and, in strips, ends at the halo.  Published rows
 // and flags live in uncached memory (hipDeviceMallocUncached): visible across the XCDs'
 // L2s without cache maintenance.  Flags carry the launch epoch, so they are never reset.
-template <int K, int NW, int W, int SYNC, bool HX, bool PG = false>
+template <int K, int NW, int W, int SYNC, bool HX, bool PG = false, bool SER = false>
 __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
                                         const StepArgs &a, WgShared<NW, PG> &sh, int tx, int y0,
                                         int y1, int nr, bool trap, int ntx)
@@ -120,8 +120,13 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     constexpr int RQ = kWgRQ, PD = kWgPD, R = kWgR;
     constexpr int U = kWgU;                              // lcm(3, RQ, R): slots are immediates
     static_assert(U % 3 == 0 && U % RQ == 0 && U % R == 0, "steady unroll");
-    constexpr int S0_ = 3 * G - 3;                       // local prologue steps
-    constexpr int EMIT0 = 3 * G - 1;                     // first local step the last stage emits
+    // SER: the wave's stages run in order within a step (stage j takes stage j-1's output of
+    // the same step), so a stage starts 2 steps after the one before it instead of 3: the
+    // pipeline fills and drains a third faster, and XS is no longer live across steps; the
+    // skewed order keeps the G stages of a step independent (ILP).  STG = steps per stage.
+    constexpr int STG = SER ? 2 : 3;
+    constexpr int S0_ = STG * G - STG;                   // local prologue steps
+    constexpr int EMIT0 = STG * G - STG + 2;             // first local step the last stage emits
     constexpr int STRIDE = 62 * ND, SHIFT = ND;
     static_assert(NW >= 2 && NW <= 8 && G >= 1, "2..8 waves, every wave a stage");
     const int lane = threadIdx.x & 63;
@@ -355,7 +360,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     auto publish = [&](auto Jc, int l, const uint32_t (&o)[ND]) {
         constexpr int jl = decltype(Jc)::value;
         if constexpr (PG && jl < NS) {
-            const int e = l - 3 * jl - 2;                // a constant in the steps that publish
+            const int e = l - STG * jl - 2;              // a constant in the steps that publish
             if ((e == 0 || e == 1) && pub_ok) buf_store(o, rx, pub_b, rowb(J + jl, e));
         }
     };
@@ -410,7 +415,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
         constexpr int XF = decltype(XFc)::value;
         using Pc = std::integral_constant<int, P>;
         unroll_seq(std::make_integer_sequence<int, JB - JA>{}, [&](auto I) {
-            constexpr int j = JB - 1 - decltype(I)::value;
+            constexpr int j = SER ? JA + decltype(I)::value : JB - 1 - decltype(I)::value;
             using RULE = std::integral_constant<bool, (j < JR)>;
             constexpr int SUBR = (XF >> j) & 1 ? 0 : (XF >> (8 + j)) & 1 ? 1 : -1;
             uint32_t x[ND];
@@ -466,7 +471,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
             ++ry;
         }
         if constexpr (PG && (XF & XPUB) != 0)
-            if (l == 3 * G) publish_flags();
+            if (l == STG * (G - 1) + 3) publish_flags();
     };
     using Tt = std::true_type;
     using Ft = std::false_type;
@@ -483,8 +488,8 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     }
     unroll_seq(std::make_integer_sequence<int, S0_>{}, [&](auto Sc) {
         constexpr int s = decltype(Sc)::value;
-        constexpr int JB = s / 3 + 1;
-        constexpr int JR = s >= 2 ? (s - 2) / 3 + 1 : 0;
+        constexpr int JB = s / STG + 1;
+        constexpr int JR = s >= 2 ? (s - 2) / STG + 1 : 0;
         step(std::integral_constant<int, s % U>{}, Z{}, std::integral_constant<int, JB>{},
              std::integral_constant<int, JR>{}, Tt{}, s, XP{});
     });
@@ -539,21 +544,22 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
         }
         if (pgt && pf < l0) take_rows();
         constexpr int GS = LAST ? G - 1 : G;             // stages that substitute
-        unroll_seq(std::make_integer_sequence<int, 3 * G - 1>{}, [&](auto Ec) {
+        unroll_seq(std::make_integer_sequence<int, STG * G - STG + 2>{}, [&](auto Ec) {
             constexpr int ep = decltype(Ec)::value;
-            constexpr int js = ep / 3, r = ep % 3;
+            constexpr int js = ep / STG, r = ep % STG;
             constexpr int XF = (js < GS && r < 2) ? (1 << (js + 8 * r)) : 0;
             // stage js >= 2: its rows were loaded 4 steps ago into the slot stage js - 2 freed
             if constexpr (r == 0 && js >= 2 && js < NS)
                 __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
             step(std::integral_constant<int, (S0_ + ep) % U>{},
-                 std::integral_constant<int, (ep + 1) / 3>{}, Gc{}, Gc{}, Ft{}, L + ep,
+                 std::integral_constant<int, SER ? ep / 2 : (ep + 1) / 3>{}, Gc{}, Gc{}, Ft{},
+                 L + ep,
                  std::integral_constant<int, XF>{});
-            if constexpr (r == 2 && js + 2 < NS)
+            if constexpr (r == STG - 1 && js + 2 < NS)
                 if (pgt) nb_load(js + 2);
         });
     } else {
-        const int l_end = nl + G - 1;
+        const int l_end = SER ? nl : nl + G - 1;
         for (int l = l0; l < l_end; l += U) {
             unroll_seq(std::make_integer_sequence<int, U>{}, [&](auto Ic) {
                 constexpr int i = decltype(Ic)::value;
@@ -580,7 +586,8 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     }
 }
 
-template <int K, int NW, int SYNC = 2, int MINW = 1, bool HX = false, bool PG = false>
+template <int K, int NW, int SYNC = 2, int MINW = 1, bool HX = false, bool PG = false,
+          bool SER = false>
 __global__ __launch_bounds__(64 * NW, MINW) void k_step_wg(const uint64_t *__restrict__ in,
                                                    uint64_t *__restrict__ out, StepArgs a,
                                                    int ntx)
@@ -608,14 +615,14 @@ __global__ __launch_bounds__(64 * NW, MINW) void k_step_wg(const uint64_t *__res
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     switch (wave) {
-    case 0: wg_wave<K, NW, 0, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
-    case 1: wg_wave<K, NW, 1, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
-    case 2: if constexpr (NW > 2) wg_wave<K, NW, 2, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
-    case 3: if constexpr (NW > 3) wg_wave<K, NW, 3, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
-    case 4: if constexpr (NW > 4) wg_wave<K, NW, 4, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
-    case 5: if constexpr (NW > 5) wg_wave<K, NW, 5, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
-    case 6: if constexpr (NW > 6) wg_wave<K, NW, 6, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
-    default: if constexpr (NW > 7) wg_wave<K, NW, 7, SYNC, HX, PG>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 0: wg_wave<K, NW, 0, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 1: wg_wave<K, NW, 1, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 2: if constexpr (NW > 2) wg_wave<K, NW, 2, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 3: if constexpr (NW > 3) wg_wave<K, NW, 3, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 4: if constexpr (NW > 4) wg_wave<K, NW, 4, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 5: if constexpr (NW > 5) wg_wave<K, NW, 5, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    case 6: if constexpr (NW > 6) wg_wave<K, NW, 6, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
+    default: if constexpr (NW > 7) wg_wave<K, NW, 7, SYNC, HX, PG, SER>(in, out, a, sh, tx, y0, y1, nr, trap, ntx); break;
     }
 }
 

@@ -34,6 +34,8 @@ static void *wg_fn(int turns, int variant)
     case kMultiWgDiag: return turns == 8 || turns == 16 ? wg_fn_nw<4, 3>(turns) : nullptr;
     case kMultiWgHx: return wg_hx_kernel(turns, false);
     case kMultiWgPg: return wg_hx_kernel(turns, true);
+    case kMultiWgHxS: return wg_ser_kernel(turns, false);
+    case kMultiWgPgS: return wg_ser_kernel(turns, true);
     default: return turns >= 13 ? wg_fn_nw<4, 2, 7>(turns) : wg_fn_nw<4, 2, 8>(turns);
     }
 }

@@ -169,7 +169,7 @@ def test_temporal_blocking_variants(gol, oracle, monkeypatch, mv, tpl, w, h, ban
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("mv", [8, 9, 12])
+@pytest.mark.parametrize("mv", [8, 9, 12, 13, 14])
 @pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 19), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (2048, 300, 137, 37),
@@ -177,7 +177,8 @@ def test_temporal_blocking_variants(gol, oracle, monkeypatch, mv, tpl, w, h, ban
                                             (4096, 1000, 250, 48), (1024, 17, 1000, 33),
                                             (256, 200, 23, 21), (1920, 130, 5, 18),
                                             (256, 200, 40, 21), (1920, 333, 37, 18),
-                                            (8064, 130, 43, 40), (2048, 500, 67, 33)])
+                                            (8064, 130, 43, 40), (2048, 500, 67, 33),
+                                            (2048, 500, 48, 33), (1920, 333, 50, 18)])
 def test_temporal_blocking_workgroup(gol, oracle, monkeypatch, mv, tpl, w, h, band, turns):
     """k_step_wg (one band's K-stage pipeline split over the 4 (2) waves of a workgroup, rows
     handed on through LDS, K up to 16) is bit-exact for every depth: bands shorter than K,
@@ -186,7 +187,9 @@ def test_temporal_blocking_workgroup(gol, oracle, monkeypatch, mv, tpl, w, h, ba
     row wrap as in-tile halo words, a short last band: 200 = 8 x 23 + 16, 130 = 26 x 5);
     mv 12 = helix with parallelogram bands (rows published by the band below, the last
     band's tiles as trapezoids) where golk::pg_ok allows it (K = 4, 12 with bands 40, 64,
-    250, 1000; K = 8, 16 with 37, 43, 67; 130 = 3 x 43 + 1), else plain helix."""
+    250, 1000; K = 8, 16 with 37, 43, 67; 130 = 3 x 43 + 1), else plain helix; mv 13 / 14 =
+    mv 9 / 12 with each wave's stages in order within a step (parallelogram bands at K = 4,
+    16 with 40, 64, 250, 1000; K = 8 with 48; K = 12 with 50)."""
     monkeypatch.setenv("GOL_MULTI_VARIANT", str(mv))
     start = oracle.gen_random(tpl * 13 + w + h, w, h)
     with _engine(gol, w, h, band_rows=band, turns_per_launch=tpl) as e:
@@ -247,7 +250,7 @@ def test_launch_planner(gol, oracle):
     assert np.array_equal(got, oracle.bit_run(board, w, 68))
 
 
-@pytest.mark.parametrize("mv", [8, 9, 12])
+@pytest.mark.parametrize("mv", [8, 9, 12, 13, 14])
 @pytest.mark.parametrize("key", ["16384x16384_seed2_t10000", "65536x65536_seed3_t1000"])
 def test_large_board_digests_workgroup(gol, monkeypatch, mv, key):
     """k_step_wg (autotuned K and band; band or helix tiling) at the BASELINE sizes vs the
@@ -328,7 +331,7 @@ def test_interleaved_raw_layout(gol, oracle, monkeypatch):
     assert np.array_equal(bot.cpu().numpy().view(np.uint64), got[rows - K:])
 
 
-@pytest.mark.parametrize("mv", [7, 8, 9, 12])
+@pytest.mark.parametrize("mv", [7, 8, 9, 12, 13, 14])
 @pytest.mark.parametrize("n,K,tpl", [(2, 8, 4), (3, 5, 4), (4, 6, 8), (1, 7, 3), (2, 20, 16),
                                      (3, 16, 12), (2, 40, 32), (3, 30, 24)])
 def test_temporal_blocking_strips(gol, oracle, monkeypatch, mv, n, K, tpl):
