@@ -18,10 +18,16 @@ Printed (rank 0): one JSON line with the driver's contract fields plus
 write of the packed board, 0.25/k B per cell-update for k fused turns -- per average
 launch time, vs 8 TB/s; PMC-measured bytes in `traffic`), `k1_equivalent` (the k = 1
 bytes of SURVEY 8(d), which exceed any HBM roof once k > 1), `valu_roofline` (the
-binding roof of the blocked kernel), `configs_measured` (BASELINE configs[2]: the
-16384^2 board, 10000 turns, same N) and `cpu_baseline` (oracle/refcpu.c, the C
-restatement of the reference's CPU path, timed on a bounded sample on this host's CPU
-share).
+binding roof of the blocked kernel), `configs_measured` and `cpu_baseline`:
+  * configs_measured: BASELINE configs[2] (16384^2, 10000 turns, same N); at N = 1
+    configs[1] (5120^2 seed 1, 1000 turns, with the final AliveCellsCount snapshot inside
+    the timed region) and configs[0] on the GPU (the reference's 512^2 image, 100 turns,
+    checked byte-exact against Local/check/images/512x512x100.pgm); at N > 1, when the
+    headline's timed turns hold no halo exchange (the driver's 20 turns < halo 128), the
+    same board again over enough turns to time >= 2 exchanges (`exchanges_timed`).
+  * cpu_baseline: oracle/refcpu.c, the C restatement of the reference's CPU path, on a
+    bounded sample of the headline board on this host's CPU share, plus configs[0] in full
+    (512^2 x 100 turns, Threads = 8) checked byte-exact against the same golden image.
 """
 import argparse
 import json
@@ -73,6 +79,14 @@ def parse():
                          "0 = skip)")
     ap.add_argument("--c3-turns", type=int, default=10000,
                     help="turns of the second config (configs[2]: 10000)")
+    ap.add_argument("--c2-size", type=int, default=5120,
+                    help="board side of BASELINE configs[1] (N = 1 only; 0 = skip)")
+    ap.add_argument("--c2-turns", type=int, default=1000)
+    ap.add_argument("--no-c1", action="store_true",
+                    help="skip BASELINE configs[0] (512^2 image, 100 turns) on GPU and CPU")
+    ap.add_argument("--exchange-turns", type=int, default=0,
+                    help="N > 1: turns of the extra measurement that times halo exchanges "
+                         "(0 = 2 x halo + 20, run only when the headline timed none)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="N > 1, direct RCCL: 1 = overlap the halo exchange with the first "
                          "launch's interior rows (gol_step_overlap, RCCL on its own stream); "
@@ -133,9 +147,13 @@ def cpu_baseline(size, seed, turns, cores):
                       f"{omp}; no gob/HTTP: optimistic), {dt:.1f} s"}
 
 
-def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
+def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed=None,
+            snapshot=False):
     """Time `steps` turns of one size x size torus board (whole board at N = 1, this rank's
-    row strip at N > 1) after `warmup` turns.  Returns the timing and roofline inputs."""
+    row strip at N > 1) after `warmup` turns.  `snapshot`: the AliveCellsCount pair of the
+    final turn (gol_snapshot) is taken inside the timed region.  Returns the timing and
+    roofline inputs."""
+    seed = a.seed if seed is None else seed
     import gol
     from gol.distributed import DistStrip, EngineStrip, make_engine_strip
 
@@ -144,14 +162,14 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
     if world == 1:
         eng = gol.Engine(W, H, device=gpu, band_rows=a.band, turns_per_launch=a.tpl)
         eng.set_stream(stream.cuda_stream)
-        eng.fill_random(a.seed)
+        eng.fill_random(seed)
         runner = eng
         rows_local = H
         transport = ""
     else:
         eng = make_engine_strip(W, H, rank, world, a.halo, gpu, band_rows=a.band,
                                 turns_per_launch=a.tpl)
-        eng.fill_random(a.seed)
+        eng.fill_random(seed)
         transport = a.transport
         if a.backend == "nccl" and transport == "rccl":
             from gol.rccl import RcclComm
@@ -176,6 +194,7 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
     ev0.record(stream)
     ev1.record(stream)
     launches0 = eng.info().launches
+    exchanges0 = getattr(runner, "exchanges", 0)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier(device_ids=dev_ids)
@@ -185,6 +204,7 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
     ev0.record(stream)
     runner.step(steps)
     ev1.record(stream)
+    alive = eng.snapshot() if snapshot else None
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier(device_ids=dev_ids)
@@ -194,6 +214,7 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
     plan = eng.last_launches()          # the last gol_step call's launches (N > 1: one window)
     info = eng.info()
     launches = info.launches - launches0
+    exchanges = getattr(runner, "exchanges", 0) - exchanges0
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64,
                          device=dev if a.backend == "nccl" else "cpu")
@@ -205,7 +226,8 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream):
     out = {"W": W, "H": H, "steps": steps, "wall": wall, "gpu_ms": gpu_ms,
            "launches": launches, "K": info.turns_per_launch, "rows_local": rows_local,
            "band": info.band_rows, "fast": bool(info.fast_path), "halo": info.halo,
-           "transport": transport, "overlap": overlap, "plan": plan}
+           "transport": transport, "overlap": overlap, "plan": plan, "seed": seed,
+           "exchanges": exchanges, "alive": alive}
     eng.close()
     return out
 
@@ -214,7 +236,89 @@ KERNELS = {7: "k_step_skew<K> (interleaved layout, one pipeline per wave)",
            8: "k_step_wg<K> (pipeline split over a workgroup, band tiles)",
            9: "k_step_wg<K> (pipeline split over a workgroup, helix tiles)",
            12: "k_step_wg<K> (helix tiles, parallelogram bands)",
+           13: "k_step_wg<K> (helix tiles, in-order stages)",
+           14: "k_step_wg<K> (parallelogram bands, in-order stages)",
+           15: "k_step_tile<K> (2-D tile resident in registers, small boards)",
            0: "k_step_ring<D=3> (one turn per launch)"}
+
+
+def kernel_depth(plan, default):
+    """(run-length summary, dominant kernel id, its deepest planned launch)."""
+    text, kvar = plan_summary(plan)
+    return text, kvar, max((k for k, v, _ in plan if v == kvar), default=default)
+
+
+def config_entry(c, label, world, parallel):
+    """configs_measured entry: GCUPS, launch plan, roofline fractions of one measure()."""
+    g = c["W"] * c["H"] * c["steps"] / c["wall"] / 1e9
+    lu = c["gpu_ms"] * 1e3 / max(c["launches"], 1)
+    b = BYTES_PER_CELL_UPDATE * c["rows_local"] * c["W"]
+    text, kvar, kd = kernel_depth(c["plan"], c["K"])
+    traffic, src = pmc_traffic(c["W"], kd)
+    e = {"workload": label, "value": round(g, 2), "unit": "GCUPS", "n_gpus": world,
+         "ms_per_step": round(c["wall"] * 1e3 / c["steps"], 6), "parallelism": parallel,
+         "band_rows": c["band"], "temporal_blocking_k": kd,
+         "kernel": KERNELS.get(kvar, f"kernel {kvar}").replace("<K>", f"<K={kd}>"),
+         "launch_plan": text[:300], "traffic": traffic, "traffic_source": src,
+         "launch_us": round(lu, 3), "launches": c["launches"],
+         "roofline_frac": round(b / (lu * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+         "valu_roofline_frac": round(g / world / VALU_PEAK_GCUPS, 4)}
+    if world > 1:
+        e["exchanges_timed"] = c["exchanges"]
+    if c.get("alive") is not None:
+        e["alive_cells_final"] = list(c["alive"])
+    return e
+
+
+def measure_c1(gpu, stream):
+    """BASELINE configs[0] on the GPU: the reference's Local/images/512x512.pgm, 100 turns,
+    gol_load -> gol_step -> gol_read_board, byte-compared with Local/check/images/
+    512x512x100.pgm (tests/golden fixtures).  Timed from the loaded board to the read-back
+    bytes (one warm run first)."""
+    import numpy as np
+    import gol
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import golden_data as G
+    board, want = G.input_board(512), G.check_board(512, 100)
+    eng = gol.Engine(512, 512, device=gpu)
+    eng.set_stream(stream.cuda_stream)
+    best, exact = None, True
+    for _ in range(3):
+        eng.load(board)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.step(100)
+        got = eng.read_board()
+        dt = time.perf_counter() - t0
+        exact = exact and bool(np.array_equal(got, want))
+        best = dt if best is None else min(best, dt)
+    plan = eng.last_launches()
+    eng.close()
+    return {"workload": "512x512 Local/images/512x512.pgm, 100 turns (BASELINE configs[0]) "
+                        "on the GPU, load excluded, read-back of the 0/255 bytes included",
+            "value": round(512 * 512 * 100 / best / 1e9, 3), "unit": "GCUPS", "n_gpus": 1,
+            "ms_per_step": round(best * 1e3 / 100, 6), "launch_plan": plan_summary(plan)[0],
+            "bit_exact_vs_check_image": exact, "best_of": 3}
+
+
+def cpu_c1(cores_note):
+    """BASELINE configs[0] on the CPU in full: oracle/refcpu.c (the reference's byte-per-cell
+    calculateNextState with its Server strip split and SubServer thread split), Threads = 8
+    on 8 OpenMP threads, 100 turns of the 512^2 image, byte-compared with the golden."""
+    import numpy as np
+    from oracle import oracle as O
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import golden_data as G
+    board, want = G.input_board(512), G.check_board(512, 100)
+    t0 = time.perf_counter()
+    got = O.ref_run(board, 100, nsub=4, threads=8, ncores=8)
+    dt = time.perf_counter() - t0
+    return {"value": round(512 * 512 * 100 / dt / 1e9, 4), "unit": "GCUPS", "cores": 8,
+            "kind": "port", "seconds": round(dt, 4),
+            "bit_exact_vs_check_image": bool(np.array_equal(got, want)),
+            "sample": "BASELINE configs[0] in full: Local/images/512x512.pgm, 100 turns, "
+                      "oracle/refcpu.c with 4 sub-servers x Threads=8 on 8 OpenMP threads "
+                      f"({cores_note}; no gob/HTTP: optimistic)"}
 
 
 def plan_summary(plan):
@@ -267,11 +371,26 @@ def main():
     stream.synchronize()
     _ = stream.cuda_stream
 
+    if a.backend == "gloo" and world > max(torch.cuda.device_count(), 1):
+        # ranks share a GPU: no parallelogram bands (their cross-workgroup waits assume one
+        # grid per device at a time; the engine cannot see other processes' grids)
+        os.environ["GOL_SHARED_DEVICE"] = "1"
     m = measure(a, a.size, a.steps, a.warmup, world, rank, gpu, dev, dev_ids, stream)
+    mx = None
+    if world > 1 and m["exchanges"] == 0:
+        # the driver's 20 timed turns fit inside one halo window: time the same board again
+        # over >= 2 exchanges so RCCL / xGMI time is in a reported number
+        xt = a.exchange_turns or 2 * m["halo"] + 20
+        mx = measure(a, a.size, xt, a.warmup, world, rank, gpu, dev, dev_ids, stream)
     c3 = None
     if a.c3_size > 0 and a.c3_size != a.size:
         c3 = measure(a, a.c3_size, a.c3_turns, max(a.warmup, 60), world, rank, gpu, dev,
                      dev_ids, stream)
+    c2 = None
+    if world == 1 and a.c2_size > 0 and a.c2_size != a.size:
+        c2 = measure(a, a.c2_size, a.c2_turns, max(a.warmup, 64), world, rank, gpu, dev,
+                     dev_ids, stream, seed=1, snapshot=True)
+    c1 = measure_c1(gpu, stream) if world == 1 and not a.no_c1 else None
 
     if rank == 0:
         W, H, K = m["W"], m["H"], m["K"]
@@ -290,8 +409,7 @@ def main():
         bytes_board = BYTES_PER_CELL_UPDATE * cells_local
         bytes_k1 = BYTES_PER_CELL_UPDATE * turns_per_launch * cells_local
         achieved = bytes_board / (launch_us * 1e-6) / 1e9
-        plan_text, kvar = plan_summary(m["plan"])
-        kdepth = max((k for k, v, _ in m["plan"] if v == kvar), default=K)
+        plan_text, kvar, kdepth = kernel_depth(m["plan"], K)
         traffic, traffic_src = pmc_traffic(W, kdepth)
         out = {
             "metric": METRIC,
@@ -307,12 +425,12 @@ def main():
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": f"{W}x{H} random torus board (seed {a.seed}), "
-                                   f"{a.steps} turns, bit-packed stencil, up to {K} turns "
+                                   f"{a.steps} turns, bit-packed stencil, up to {kdepth} turns "
                                    f"per launch",
                        "board": [W, H], "turns": a.steps,
                        "parallelism": parallelism(a, world, m),
                        "band_rows": m["band"], "fast_path": m["fast"],
-                       "temporal_blocking_k": K,
+                       "temporal_blocking_k": kdepth,
                        "launch_plan": plan_text},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -343,25 +461,33 @@ def main():
                 "model": "52 SIMD cycles per 4096 cell-updates (18 full-rate v_bitop3 + 4 "
                          "half-rate v_alignbit/DPP), 1024 SIMDs x 2.4 GHz; useful cell-updates "
                          "only (halo lanes, band halos and pipeline fill count against it)"}
+        if world > 1:
+            out["config"]["exchanges_timed"] = m["exchanges"]
+        cm = []
+        if mx is not None:
+            cm.append(config_entry(mx, f"{W}x{H} random torus board (seed {a.seed}), "
+                                       f"{mx['steps']} turns: the headline board timed over "
+                                       f"{mx['exchanges']} halo exchanges", world,
+                                   parallelism(a, world, mx)))
         if c3 is not None:
-            g3 = c3["W"] * c3["H"] * c3["steps"] / c3["wall"] / 1e9
-            l3 = c3["gpu_ms"] * 1e3 / max(c3["launches"], 1)
-            b3 = BYTES_PER_CELL_UPDATE * c3["rows_local"] * c3["W"]
-            out["configs_measured"] = [{
-                "workload": f"{c3['W']}x{c3['H']} random torus board (seed {a.seed}), "
-                            f"{c3['steps']} turns (BASELINE configs[2])",
-                "value": round(g3, 2), "unit": "GCUPS", "n_gpus": world,
-                "ms_per_step": round(c3["wall"] * 1e3 / c3["steps"], 5),
-                "parallelism": parallelism(a, world, c3),
-                "band_rows": c3["band"], "temporal_blocking_k": c3["K"],
-                "launch_plan": plan_summary(c3["plan"])[0][:300],
-                "traffic": pmc_traffic(c3["W"], c3["K"])[0],
-                "traffic_source": pmc_traffic(c3["W"], c3["K"])[1],
-                "launch_us": round(l3, 2), "launches": c3["launches"],
-                "roofline_frac": round(b3 / (l3 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "valu_roofline_frac": round(g3 / world / VALU_PEAK_GCUPS, 4)}]
+            cm.append(config_entry(c3, f"{c3['W']}x{c3['H']} random torus board (seed "
+                                       f"{a.seed}), {c3['steps']} turns (BASELINE configs[2])",
+                                   world, parallelism(a, world, c3)))
+        if c2 is not None:
+            cm.append(config_entry(c2, f"{c2['W']}x{c2['H']} random torus board (seed 1), "
+                                       f"{c2['steps']} turns + the final AliveCellsCount "
+                                       f"snapshot (BASELINE configs[1])",
+                                   world, parallelism(a, world, c2)))
+        if c1 is not None:
+            cm.append(c1)
+        if cm:
+            out["configs_measured"] = cm
         if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(W, a.seed, a.cpu_turns, a.cpu_cores)
+            if not a.no_c1:
+                share, aff, omp = cpu_share()
+                out["cpu_baseline"]["c1"] = cpu_c1(f"host CPU share {share} of an affinity "
+                                                   f"mask of {aff}")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -215,7 +215,7 @@ __device__ __forceinline__ uint32_t vec_make(const uint32_t (&c)[1]) { return c[
 // 64 words in order (read back as one ds_read_b64 per lane).
 constexpr bool is_il_variant(int v)
 {
-    return v == kMultiSkewIL || v == kMultiSkewILW16 || is_wg_variant(v);
+    return v == kMultiSkewIL || v == kMultiSkewILW16 || is_wg_variant(v) || v == kMultiTile;
 }
 
 // kernel entry points built in their own translation units (parallel builds)

@@ -18,10 +18,14 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -46,6 +50,13 @@ struct Launch {
 };
 constexpr int kPlanMax = 128;               // launch plans cover gol_step / halo windows up to this
 constexpr size_t kLastCap = 4096;           // gol_last_launches records at most this many
+
+// a read-only call (gol_snapshot, gol_read_*, ...) run by a stepping thread at a launch boundary
+struct Job {
+    std::function<int()> fn;
+    int rc = 0;
+    bool done = false;
+};
 
 struct gol_ctx {
     gol_config cfg{};
@@ -97,8 +108,24 @@ struct gol_ctx {
     std::atomic<bool> control_used{false};
     std::atomic<long long> progress{0};      // lock-free mirror of `turn` (gol_get_progress)
     std::atomic<bool> parked{false};         // gol_step is parked on GOL_CONTROL_PAUSE
+    // k_step_tile shape (kMultiTile): tile width in words, rows per lane segment (the tile
+    // height is the launch's band)
+    int tile_w = 0, tile_seg = 0;
+    // device error word (host-mapped pinned memory; golk::kDevErr*): a k_step_wg wait that gave
+    // up writes it, every synchronising call checks it
+    unsigned *h_err = nullptr, *d_err = nullptr;
+    bool registered = false;                 // counted in g_dev_engines
+    hipEvent_t ev_copy = nullptr;            // gol_copy_halo_from_*: ordering between engines
     std::string err;
-    std::recursive_mutex mu;
+    std::recursive_mutex mu;                 // engine state; held by gol_step except while parked
+    // read-only calls from other threads while gol_step runs (run_read): served by the stepping
+    // thread at its next launch boundary
+    std::mutex jm;
+    std::condition_variable jcv;
+    std::vector<Job *> jobs;
+    bool stepping = false;                   // (under jm) a gol_step holds `mu`
+    std::atomic<bool> jobs_pending{false};
+    std::atomic<bool> readers{false};        // a reader was served during a step: keep the queue short
 };
 
 namespace {
@@ -138,7 +165,102 @@ struct DeviceGuard {
     }
 };
 
+// engines alive per device in this process: kMultiWgPg runs only on a device with one engine
+// (two concurrent parallelogram grids can each fill an XCD with tiles waiting for tiles of
+// their own launch that sit undispatched behind the other grid's: the waits would time out),
+// and not at all when GOL_SHARED_DEVICE is set (other processes share the GPU: torchrun ranks
+// on one device).  The rows it would have published are recomputed as plain helix bands.
+std::mutex g_dev_mu;
+std::map<int, int> g_dev_engines;
+
+bool device_exclusive(int dev)
+{
+    static const bool shared = getenv("GOL_SHARED_DEVICE") && atoi(getenv("GOL_SHARED_DEVICE"));
+    if (shared) return false;
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    auto it = g_dev_engines.find(dev);
+    return it == g_dev_engines.end() || it->second <= 1;
+}
+
 bool is_strip(const gol_ctx *c) { return c->cfg.halo > 0; }
+
+// The device error word after a synchronisation: a k_step_wg hand-off or parallelogram flag
+// wait gave up (a preempted or starved workgroup), so the board of that launch is wrong.  The
+// word stays set until the board is replaced (gol_load*, gol_fill_random): every synchronising
+// call reports it (the reference ignored its RPC errors, Server/gol/distributor.go:219).
+int check_dev_err(gol_ctx *c)
+{
+    const unsigned e = c->h_err ? *(volatile unsigned *)c->h_err : 0u;
+    if (!e) return GOL_OK;
+    return fail(c, GOL_EHIP,
+                "a k_step_wg %s wait timed out (device error word %u): the board is corrupt; "
+                "reload it", e == golk::kDevErrPgFlag ? "parallelogram flag" : "hand-off", e);
+}
+
+int sync_checked(gol_ctx *c)
+{
+    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    return check_dev_err(c);
+}
+
+void clear_dev_err(gol_ctx *c)
+{
+    if (c->h_err) *(volatile unsigned *)c->h_err = 0u;
+}
+
+// Serve the read-only calls posted by run_read (the stepping thread, holding `mu`).
+void serve_jobs(gol_ctx *c)
+{
+    std::vector<Job *> js;
+    {
+        std::lock_guard<std::mutex> jl(c->jm);
+        js.swap(c->jobs);
+        c->jobs_pending.store(false);
+    }
+    for (Job *j : js) {
+        const int rc = j->fn();
+        std::lock_guard<std::mutex> jl(c->jm);
+        j->rc = rc;
+        j->done = true;                      // (j lives on the waiter's stack: not touched again)
+    }
+    if (!js.empty()) c->jcv.notify_all();
+}
+
+void set_stepping(gol_ctx *c, bool on)
+{
+    std::lock_guard<std::mutex> jl(c->jm);
+    c->stepping = on;
+}
+
+// Run a read-only engine call.  No gol_step in progress: now, under the engine lock.  While
+// another thread's gol_step runs: by that thread at its next launch boundary, on the board the
+// step has enqueued so far (turn-consistent), so AliveCellsCount / GetWorld never wait for
+// the whole step -- the reference's Alivecount and GetWorld take the Server mutex only around
+// the per-turn commit (Server/gol/distributor.go:62-75,131-134).  While the step is parked on
+// PAUSE it has released the engine, and the call runs now.
+template <class F>
+int run_read(gol_ctx *c, F &&fn)
+{
+    for (;;) {
+        std::unique_lock<std::mutex> jl(c->jm);
+        if (c->stepping) {
+            Job j;
+            j.fn = std::function<int()>(fn);
+            c->jobs.push_back(&j);
+            c->jobs_pending.store(true);
+            c->readers.store(true);
+            c->jcv.wait(jl, [&] { return j.done; });
+            return j.rc;
+        }
+        if (c->mu.try_lock()) {              // (the owner of a recursive lock gets it too)
+            jl.unlock();
+            std::lock_guard<std::recursive_mutex> lk(c->mu, std::adopt_lock);
+            return fn();
+        }
+        jl.unlock();                         // a short call holds the engine, or a step is
+        std::this_thread::sleep_for(std::chrono::microseconds(50));   // about to flag itself
+    }
+}
 
 // rows of the owned region inside the buffer
 int own_lo(const gol_ctx *c) { return c->cfg.halo; }
@@ -188,7 +310,8 @@ int ensure_layout(gol_ctx *c, bool il)
 // band it runs at).
 int band_same_rounds(const gol_ctx *c, int var, int K0, int band0, int k)
 {
-    if (k == K0 || k < 2 || k > golk::kMaxTurnsPerLaunch) return band0;
+    if (k == K0 || k < 2 || k > golk::kMaxTurnsPerLaunch || var == golk::kMultiTile)
+        return band0;                        // (k_step_tile: the tile height stays)
     const int lane_dw = golk::multi_lane_dwords(c->multi_words, var);
     const int per = golk::multi_pipes_per_block(var);
     const long long cap_t = (long long)c->ncu * golk::multi_blocks_per_cu(K0, c->multi_words, var) * per;
@@ -267,7 +390,7 @@ int count_now(gol_ctx *c, long long *alive)
                                          slot, c->stream));
     HIP_OR_FAIL(c, hipMemcpyAsync(c->h_counts, slot, kShards * sizeof(unsigned long long),
                                   hipMemcpyDeviceToHost, c->stream));
-    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+    if (int rc = sync_checked(c)) return rc;
     unsigned long long s = 0;
     for (int i = 0; i < kShards; i++) s += c->h_counts[i];
     *alive = (long long)s;
@@ -284,6 +407,11 @@ static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
     if (!golk::is_pg_variant(a.multi_variant) ||
         !golk::pg_ok(k, a.band, a.multi_variant == golk::kMultiWgPgS))
         return hipSuccess;
+    if (!device_exclusive(c->device)) {      // (launch_wg runs it as plain helix bands)
+        a.multi_variant = a.multi_variant == golk::kMultiWgPgS ? golk::kMultiWgHxS
+                                                               : golk::kMultiWgHx;
+        return hipSuccess;
+    }
     const long long T =
         golk::multi_pipes(a.width, a.row_hi - a.row_lo, a.band, 2, a.multi_variant);
     const size_t lanes = (size_t)T * 62 + 64;
@@ -315,6 +443,137 @@ static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
     a.xlanes = (unsigned)c->pg_lanes;
     a.epoch = ++c->pg_epoch;
     return hipSuccess;
+}
+
+// ---------------------------------------------------------------- k_step_tile planning
+struct TileShape {
+    int K = 0, th = 0, tw = 0, seg = 0;
+    double model_us = 0;                     // modelled time per turn
+};
+
+// Modelled time per turn of k_step_tile at one shape: per turn a wave
+// issues (SEG + 2) row sums (2 DPP + 2 v_alignbit at 4 cycles, 4 v_bitop3 at 2: 24 cycles)
+// and SEG rules (14 v_bitop3: 28 cycles); a SIMD issues its resident waves' work back to back
+// but one wave alone runs ~2.5x slower than issue (dependent VALU latency, calibrated by
+// tools/calib/valu_issue.hip); each turn adds a barrier, each launch its tile load and a
+// launch gap.
+double tile_model_us(int ncu, int nw, int rows, int K, int th, int tw, int seg)
+{
+    if (!golk::tile_shape_ok(nw, K, th, tw, seg)) return 0;
+    const long long tiles = golk::tile_count(nw, rows, th, tw);
+    const int waves = golk::tile_waves(K, th, tw, seg);
+    const int wgpc = std::max(1, std::min(32 / waves, 4));            // waves / CU, LDS
+    const long long slots = (long long)ncu * wgpc;
+    const long long rounds = (tiles + slots - 1) / slots;
+    const long long per_cu = std::min<long long>((tiles + ncu - 1) / ncu, wgpc);
+    const double wps = (double)(per_cu * waves) / 4.0;                 // waves per SIMD
+    const double cyc_wave = (seg + 2) * 24.0 + seg * 28.0;
+    const double turn_cyc = std::max(std::ceil(wps), 2.5) * cyc_wave + 150.0;
+    const double launch_us = rounds * (K * turn_cyc + 2500.0) / 2400.0 + 3.0;
+    return launch_us / K;
+}
+
+// The shapes the model ranks best for a board of nw words x rows (one per (K, TW), best TH
+// and SEG), fastest first.
+std::vector<TileShape> tile_candidates(int ncu, int nw, int rows, int keep)
+{
+    std::vector<TileShape> all;
+    std::vector<int> tws;
+    for (int ntx = 1; ntx <= nw; ++ntx) {
+        const int tw = (nw + ntx - 1) / ntx;
+        if (tw <= 62 && (tws.empty() || tws.back() != tw)) tws.push_back(tw);
+    }
+    for (int K : {8, 12, 16, 20, 24, 32}) {
+        for (int tw : tws) {
+            TileShape best;
+            const long long ntx = (nw + tw - 1) / tw;
+            for (int per_cu : {1, 2, 3, 4}) {
+                const long long nty = std::max<long long>(1, ((long long)ncu * per_cu + ntx - 1) / ntx);
+                const int th = (int)std::max<long long>(1, (rows + nty - 1) / nty);
+                for (int seg : {2, 3, 4, 6, 8}) {
+                    const double m = tile_model_us(ncu, nw, rows, K, th, tw, seg);
+                    if (m > 0 && (best.K == 0 || m < best.model_us)) best = {K, th, tw, seg, m};
+                }
+            }
+            if (best.K) all.push_back(best);
+        }
+    }
+    std::sort(all.begin(), all.end(),
+              [](const TileShape &x, const TileShape &y) { return x.model_us < y.model_us; });
+    if ((int)all.size() > keep) all.resize((size_t)keep);
+    return all;
+}
+
+void apply_tile(gol_ctx *c, const TileShape &t)
+{
+    c->multi_variant = golk::kMultiTile;
+    c->tpl = t.K;
+    c->band_multi = t.th;
+    c->tile_w = t.tw;
+    c->tile_seg = t.seg;
+    for (int &b : c->band_at) b = 0;
+    c->plan.clear();
+}
+
+// Boards below 2^20 words (5120^2: 409 600) cannot fill the GPU with band pipelines: time the
+// model's best k_step_tile shapes on the engine's own buffers and keep the fastest.
+void autotune_small(gol_ctx *c)
+{
+    std::vector<TileShape> cand = tile_candidates(c->ncu, c->nw, c->buf_rows, 24);
+    if (cand.empty()) return;
+    golk::StepArgs a{};
+    a.width = c->cfg.width;
+    a.nw = c->nw;
+    a.pitch = c->pitch;
+    a.modrows = c->buf_rows;
+    a.row_lo = 0;
+    a.row_hi = c->buf_rows;
+    a.multi_words = 1;
+    a.multi_variant = golk::kMultiTile;
+    a.err = c->d_err;
+    if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
+                                 c->buf_rows, 12345, c->stream) != hipSuccess)
+        return;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return;
+    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
+    auto time_one = [&](const TileShape &t, int reps) -> float {
+        a.band = t.th;
+        a.tile_w = t.tw;
+        a.tile_seg = t.seg;
+        bool ok = hipEventRecord(e0, c->stream) == hipSuccess;
+        for (int rep = 0; rep < reps && ok; ++rep) {
+            a.in = c->board[rep & 1];
+            a.out = c->board[(rep + 1) & 1];
+            ok = golk::launch_step_multi(a, t.K, c->stream) == hipSuccess;
+        }
+        ok = ok && hipEventRecord(e1, c->stream) == hipSuccess &&
+             hipEventSynchronize(e1) == hipSuccess;
+        float ms = 0.f;
+        if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return 0.f;
+        return ms / ((float)reps * t.K);
+    };
+    (void)time_one(cand[0], 40);             // clock ramp
+    std::vector<float> t(cand.size(), 0.f);
+    for (int pass = 0; pass < 2; ++pass)
+        for (size_t i = 0; i < cand.size(); ++i) {
+            const float v = time_one(cand[i], 16);
+            if (v > 0.f && (t[i] == 0.f || v < t[i])) t[i] = v;
+        }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipGetLastError();
+    int bi = -1;
+    for (size_t i = 0; i < cand.size(); ++i) {
+        if (getenv("GOL_AUTOTUNE_LOG"))
+            fprintf(stderr, "autotune tile %dx%d K=%d th=%d tw=%d seg=%d model=%.3f us=%.3f\n",
+                    c->cfg.width, c->buf_rows, cand[i].K, cand[i].th, cand[i].tw, cand[i].seg,
+                    cand[i].model_us, t[i] * 1000.f);
+        if (t[i] > 0.f && (bi < 0 || t[i] < t[(size_t)bi])) bi = (int)i;
+    }
+    if (bi < 0) return;
+    apply_tile(c, cand[(size_t)bi]);
+    c->tuned_us_per_turn = t[(size_t)bi] * 1000.f;
 }
 
 // Create-time timing sweep of the temporal-blocking kernel, its depth K and its band on
@@ -387,6 +646,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     a.variant = c->variant;
     a.multi_words = c->multi_words;
     a.wg_prio = c->wg_prio;
+    a.err = c->d_err;
     if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
                                  c->buf_rows, 12345, c->stream) != hipSuccess)
         return;
@@ -625,6 +885,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     // 87 VGPRs at K=4), K = 6 on large boards (64-row bands), K = 4 on smaller ones
     c->multi_words = 1;
     if (const char *v = getenv("GOL_MULTI_WORDS")) c->multi_words = atoi(v) == 1 ? 1 : 2;
+    if (!GOL_TOOLS && c->multi_words != 1) {  // 2 words per lane: a superseded build
+        delete c;
+        return GOL_EINVAL;
+    }
     if (const char *v = getenv("GOL_WG_PRIO")) {          // A/B experiments only: "3210" =
         for (int w = 0; w < 4 && v[w] >= '0' && v[w] <= '3'; ++w)   // wave 0..3's priority
             c->wg_prio |= (unsigned)(v[w] - '0') << (2 * w);
@@ -632,8 +896,15 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     }
     if (const char *v = getenv("GOL_MULTI_VARIANT")) {    // A/B experiments only
         const int k = atoi(v);
-        c->multi_variant = (k >= 0 && k < golk::kMultiCount) || k > golk::kMultiAblate
-                               ? k : golk::kMultiSkew;
+        const bool known = (k >= 0 && k < golk::kMultiCount) || k > golk::kMultiAblate;
+        // the product library ships only the kernels that compute the right board
+        // (multi_variant_shipped); ablations, diagnostics and superseded variants need the
+        // tools build (libgolamd_tools.so via GOL_AMD_LIB)
+        if (!known || (!GOL_TOOLS && !golk::multi_variant_shipped(k))) {
+            delete c;
+            return GOL_EINVAL;
+        }
+        c->multi_variant = k;
     }
     const int lane_dw = golk::multi_lane_dwords(c->multi_words, c->multi_variant);
     const int auto_bm = golk::auto_band_multi(cfg->width, cfg->rows, lane_dw);
@@ -673,18 +944,74 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         (e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming)) != hipSuccess) {
+        (e = hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_copy, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&c->h_err, sizeof(unsigned),
+                           hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0)) != hipSuccess) {
         rc = e == hipErrorOutOfMemory ? GOL_ENOMEM : GOL_EHIP;
         return bail(rc);
     }
+    clear_dev_err(c);
+    {
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        ++g_dev_engines[dev];
+        c->registered = true;
+    }
     c->stream = c->own_stream;
-    if (c->tpl > 1 && cfg->band_rows <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {
+    // small boards: k_step_tile (kMultiTile) at the model's best shape for the requested or
+    // default depth; the autotune below times the model's best shapes
+    const bool small = c->fast && c->tpl > 1 && (long long)c->buf_rows * c->pitch < (1ll << 20);
+    const bool pinned = getenv("GOL_MULTI_VARIANT") != nullptr;
+    if (small && ((!pinned && cfg->band_rows <= 0) || c->multi_variant == golk::kMultiTile)) {
+        int K = cfg->turns_per_launch > 0 ? std::min(cfg->turns_per_launch, 32) : 0;
+        if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) K = std::max(2, std::min(atoi(v), 32));
+        std::vector<TileShape> cand = tile_candidates(c->ncu, c->nw, c->buf_rows, 1 << 20);
+        for (const TileShape &t : cand)
+            if (K == 0 || t.K == K) {
+                apply_tile(c, t);
+                break;
+            }
+        if (K > 0 && c->multi_variant == golk::kMultiTile && c->tpl != K) {
+            // no ranked shape at this depth (K not in the candidate list): best TW / TH at K
+            TileShape best;
+            for (const TileShape &t : cand) {
+                const double m = tile_model_us(c->ncu, c->nw, c->buf_rows, K, t.th, t.tw, t.seg);
+                if (m > 0 && (best.K == 0 || m < best.model_us)) best = {K, t.th, t.tw, t.seg, m};
+            }
+            if (best.K) apply_tile(c, best);
+        }
+        if (c->multi_variant == golk::kMultiTile && cfg->band_rows > 0)
+            c->band_multi = cfg->band_rows;  // tile height pinned by the caller
+        if (const char *v = getenv("GOL_TILE")) {           // experiments: "TW,SEG"
+            int tw = 0, seg = 0;
+            if (sscanf(v, "%d,%d", &tw, &seg) == 2 && tw > 0 && seg > 0) {
+                c->multi_variant = golk::kMultiTile;
+                c->tile_w = tw;
+                c->tile_seg = seg;
+            }
+        }
+        if (c->multi_variant == golk::kMultiTile &&
+            !golk::tile_shape_ok(c->nw, c->tpl, c->band_multi, c->tile_w, c->tile_seg))
+            return bail(GOL_EINVAL);
+    } else if (c->multi_variant == golk::kMultiTile) {
+        return bail(GOL_EINVAL);             // k_step_tile: boards below 2^20 words only
+    }
+    if (small && c->multi_variant == golk::kMultiTile && !pinned && cfg->band_rows <= 0 &&
+        cfg->turns_per_launch <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {
+        const char *at = getenv("GOL_AUTOTUNE");
+        if (!at || atoi(at) != 0) autotune_small(c);
+        if (int rc2 = check_dev_err(c)) return bail(rc2);
+    } else if (c->tpl > 1 && cfg->band_rows <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {
         const char *at = getenv("GOL_AUTOTUNE");
         // the kernel is tuned too unless an experiment pins it (GOL_MULTI_VARIANT) or the
         // requested depth only one of them runs
         const bool tune_var = !getenv("GOL_MULTI_VARIANT") && c->multi_words == 1 &&
                               (cfg->turns_per_launch <= 0 || cfg->turns_per_launch <= 8);
         if (!at || atoi(at) != 0) autotune_multi(c, cfg->turns_per_launch <= 0, tune_var);
+        // a wait that gave up while timing the candidates: fail loudly at create
+        (void)hipStreamSynchronize(c->stream);
+        if (check_dev_err(c)) return bail(GOL_EHIP);
     }
     if ((e = hipMemsetAsync(c->board[0], 0, words * 8, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->board[1], 0, words * 8, c->stream)) != hipSuccess ||
@@ -699,6 +1026,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
 void gol_destroy(gol_ctx *c)
 {
     if (!c) return;
+    if (c->registered) {
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        if (--g_dev_engines[c->device] <= 0) g_dev_engines.erase(c->device);
+    }
     {
         DeviceGuard g(c->device);
         if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
@@ -716,6 +1047,8 @@ void gol_destroy(gol_ctx *c)
         if (c->side) (void)hipStreamDestroy(c->side);
         if (c->ev_side) (void)hipEventDestroy(c->ev_side);
         if (c->ev_main) (void)hipEventDestroy(c->ev_main);
+        if (c->ev_copy) (void)hipEventDestroy(c->ev_copy);
+        if (c->h_err) (void)hipHostFree(c->h_err);
     }
     delete c;
 }
@@ -723,25 +1056,26 @@ void gol_destroy(gol_ctx *c)
 int gol_get_info(gol_ctx *c, gol_info *info)
 {
     if (!c || !info) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    info->width = c->cfg.width;
-    info->height = c->cfg.height;
-    info->row_offset = c->cfg.row_offset;
-    info->rows = c->cfg.rows;
-    info->halo = c->cfg.halo;
-    info->words_per_row = c->nw;
-    info->pitch_words = c->pitch;
-    info->buffer_rows = c->buf_rows;
-    info->fast_path = c->fast ? 1 : 0;
-    info->band_rows = c->tpl > 1 ? c->band_multi : c->band;   // band of the kernel in use
-    info->halo_valid = c->halo_valid;
-    info->turns_per_launch = c->tpl;
-    info->device = c->device;
-    info->turn = c->turn;
-    info->nonbinary_cells = c->nonbinary;
-    info->launches = c->launches;
-    info->blocking_limited = c->blocking_limited ? 1 : 0;
-    return GOL_OK;
+    return run_read(c, [&]() -> int {
+        info->width = c->cfg.width;
+        info->height = c->cfg.height;
+        info->row_offset = c->cfg.row_offset;
+        info->rows = c->cfg.rows;
+        info->halo = c->cfg.halo;
+        info->words_per_row = c->nw;
+        info->pitch_words = c->pitch;
+        info->buffer_rows = c->buf_rows;
+        info->fast_path = c->fast ? 1 : 0;
+        info->band_rows = c->tpl > 1 ? c->band_multi : c->band;   // band of the kernel in use
+        info->halo_valid = c->halo_valid;
+        info->turns_per_launch = c->tpl;
+        info->device = c->device;
+        info->turn = c->turn;
+        info->nonbinary_cells = c->nonbinary;
+        info->launches = c->launches;
+        info->blocking_limited = c->blocking_limited ? 1 : 0;
+        return GOL_OK;
+    });
 }
 
 int gol_set_stream(gol_ctx *c, void *s)
@@ -762,8 +1096,7 @@ int gol_sync(gol_ctx *c)
     if (!c) return GOL_EINVAL;
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
-    return GOL_OK;
+    return sync_checked(c);
 }
 
 int gol_load(gol_ctx *c, const uint8_t *bytes)
@@ -797,6 +1130,7 @@ int gol_load(gol_ctx *c, const uint8_t *bytes)
     c->nonbinary = (long long)s;
     c->cur = 0;
     c->il = false;
+    clear_dev_err(c);                        // a new board: earlier hand-off failures are moot
     c->turn = 0;
     c->progress.store(0);
     c->launches = 0;
@@ -826,6 +1160,7 @@ int gol_load_packed(gol_ctx *c, const uint64_t *words)
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
     c->il = false;
+    clear_dev_err(c);                        // a new board: earlier hand-off failures are moot
     c->turn = 0;
     c->progress.store(0);
     c->launches = 0;
@@ -847,6 +1182,7 @@ int gol_fill_random(gol_ctx *c, uint64_t seed)
     HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
     c->il = false;
+    clear_dev_err(c);                        // a new board: earlier hand-off failures are moot
     c->turn = 0;
     c->progress.store(0);
     c->launches = 0;
@@ -858,7 +1194,8 @@ int gol_fill_random(gol_ctx *c, uint64_t seed)
 
 namespace {
 
-// Tools only (GOL_MULTI_VARIANT=kMultiWgDiag): one k_step_wg launch with per-wave wait
+#if GOL_TOOLS
+// Tools build only (GOL_MULTI_VARIANT=kMultiWgDiag): one k_step_wg launch with per-wave wait
 // timing, summarised by wave role on stderr.
 int wg_diag_launch(gol_ctx *c, golk::StepArgs a, int k)
 {
@@ -912,6 +1249,7 @@ int wg_diag_launch(gol_ctx *c, golk::StepArgs a, int k)
     fprintf(stderr, "wg_diag launch span %llu ticks of 100 MHz\n", t1max - t0min);
     return GOL_OK;
 }
+#endif  // GOL_TOOLS
 
 constexpr int kCtlDepth = 2;   // launches queued ahead while a control word is in use
 
@@ -920,7 +1258,8 @@ constexpr int kCtlDepth = 2;   // launches queued ahead while a control word is 
 // once, the rows next to the halos run on the side stream after everything queued on
 // xstream (the caller's halo receives) -- and the engine stream joins the side stream
 // before the next launch.
-int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
+int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
+              std::unique_lock<std::recursive_mutex> &lk)
 {
     if (is_strip(c) && turns > c->halo_valid)
         return fail(c, GOL_ESTATE, "strip engine: %lld turns requested, halos valid for %d",
@@ -939,8 +1278,22 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
     a.multi_words = c->multi_words;
     a.wg_prio = c->wg_prio;
     a.multi_variant = c->multi_variant;
+    a.err = c->d_err;
+    a.tile_w = c->tile_w;
+    a.tile_seg = c->tile_seg;
+    // read-only calls from other threads are served at launch boundaries from here on
+    struct Stepping {
+        gol_ctx *c;
+        explicit Stepping(gol_ctx *c_) : c(c_) { set_stepping(c, true); }
+        ~Stepping()
+        {
+            set_stepping(c, false);          // later readers take the lock themselves
+            serve_jobs(c);
+        }
+    } stepping(c);
     // control word: with a controlling thread present, keep at most kCtlDepth launches
-    // queued so a pause / stop takes effect within that many launches
+    // queued so a pause / stop takes effect within that many launches (and so does a reader:
+    // once one has been served during a step, steps keep the queue this short)
     struct EventRing {
         hipEvent_t ev[kCtlDepth] = {};
         int n = 0;
@@ -953,15 +1306,24 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
     c->last.clear();
     c->last_n = 0;
     for (int64_t t = 0; t < turns;) {
+        if (c->jobs_pending.load(std::memory_order_relaxed)) serve_jobs(c);
         if (ctl) {
             int w = c->control.load();
             if (w == GOL_CONTROL_PAUSE) {
                 // park at this launch boundary with the board complete (Server/gol/
-                // distributor.go:147-156: the turn loop blocks until the second 'p')
-                HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
+                // distributor.go:147-156: the turn loop blocks until the second 'p'); the
+                // engine is released while parked, so AliveCellsCount / GetWorld calls from
+                // other threads run at once (the reference's ticker keeps firing while paused,
+                // Local/gol/distributor.go:117-130,154-167)
+                if (int rc = sync_checked(c)) return rc;
+                set_stepping(c, false);
+                serve_jobs(c);
                 c->parked.store(true);
+                lk.unlock();
                 while ((w = c->control.load()) == GOL_CONTROL_PAUSE)
                     std::this_thread::sleep_for(std::chrono::microseconds(200));
+                lk.lock();
+                set_stepping(c, true);
                 c->parked.store(false);
             }
             if (w == GOL_CONTROL_STOP)   // quit / kill (distributor.go:143-146,157-164)
@@ -1004,9 +1366,12 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
             a.counts = nullptr;
             a.band = plan.band;
             a.multi_variant = plan.var;
+#if GOL_TOOLS
             if (c->multi_variant == golk::kMultiWgDiag && !split) {
                 if (int rc = wg_diag_launch(c, a, k)) return rc;
-            } else if (split && in_lo < in_hi) {
+            } else
+#endif
+            if (split && in_lo < in_hi) {
                 golk::StepArgs b = a;
                 // concurrent launches cannot share the published-row scratch
                 if (b.multi_variant == golk::kMultiWgPg) b.multi_variant = golk::kMultiWgHx;
@@ -1081,10 +1446,15 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
             c->blocked_pending = false;
             c->raw_turn0.clear();
         }
-        if (ctl) {   // bound the queue: wait for the launch kCtlDepth back
+        if (ctl || c->readers.load(std::memory_order_relaxed)) {
+            // bound the queue: wait for the launch kCtlDepth back
             hipEvent_t &e = ring.ev[ring.n % kCtlDepth];
-            if (ring.n >= kCtlDepth) HIP_OR_FAIL(c, hipEventSynchronize(e));
-            else HIP_OR_FAIL(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            if (ring.n >= kCtlDepth) {
+                HIP_OR_FAIL(c, hipEventSynchronize(e));
+                if (int rc = check_dev_err(c)) return rc;
+            } else {
+                HIP_OR_FAIL(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            }
             HIP_OR_FAIL(c, hipEventRecord(e, c->stream));
             ++ring.n;
         }
@@ -1101,8 +1471,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream)
 int gol_step(gol_ctx *c, int64_t turns)
 {
     if (!c || turns < 0) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    return step_impl(c, turns, nullptr);
+    std::unique_lock<std::recursive_mutex> lk(c->mu);
+    return step_impl(c, turns, nullptr, lk);
 }
 
 int gol_last_launches(gol_ctx *c, int32_t *turns, int32_t *kernel, int32_t *band, int32_t cap)
@@ -1121,10 +1491,10 @@ int gol_last_launches(gol_ctx *c, int32_t *turns, int32_t *kernel, int32_t *band
 int gol_step_overlap(gol_ctx *c, int64_t turns, void *recv_stream)
 {
     if (!c || turns < 0 || !recv_stream) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    std::unique_lock<std::recursive_mutex> lk(c->mu);
     if (!is_strip(c)) return fail(c, GOL_ESTATE, "not a strip engine");
     c->halo_valid = c->cfg.halo;   // the receives queued on recv_stream refresh the halos
-    return step_impl(c, turns, (hipStream_t)recv_stream);
+    return step_impl(c, turns, (hipStream_t)recv_stream, lk);
 }
 
 int gol_stream_wait(gol_ctx *c, void *stream)
@@ -1156,143 +1526,148 @@ int gol_get_progress(gol_ctx *c, int64_t *turn, int32_t *parked)
 int gol_snapshot(gol_ctx *c, int64_t *turn, int64_t *alive)
 {
     if (!c || !turn || !alive) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    long long n = 0;
-    int rc = count_now(c, &n);
-    if (rc) return rc;
-    *turn = c->turn;
-    *alive = n;
-    return GOL_OK;
+    return run_read(c, [&]() -> int {
+        DeviceGuard g(c->device);
+        long long n = 0;
+        int rc = count_now(c, &n);
+        if (rc) return rc;
+        *turn = c->turn;
+        *alive = n;
+        return GOL_OK;
+    });
 }
 
 int gol_turn_counts(gol_ctx *c, int64_t first_turn, int64_t n, int64_t *out)
 {
     if (!c || !out || n < 0) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    if (!(c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN))
-        return fail(c, GOL_ESTATE, "engine created without GOL_FLAG_COUNT_EVERY_TURN");
-    if (n == 0) return GOL_OK;
-    if (first_turn < 1 || first_turn + n - 1 > c->turn || first_turn <= c->turn - kRing)
-        return fail(c, GOL_EINVAL, "turns %lld..%lld not in the recorded window",
-                    (long long)first_turn, (long long)(first_turn + n - 1));
-    DeviceGuard g(c->device);
-    std::vector<unsigned long long> h((size_t)kRing * kShards);
-    HIP_OR_FAIL(c, hipMemcpyAsync(h.data(), c->counts, h.size() * 8, hipMemcpyDeviceToHost,
-                                  c->stream));
-    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
-    for (int64_t i = 0; i < n; ++i) {
-        const size_t slot = (size_t)((first_turn + i) % kRing);
-        unsigned long long s = 0;
-        for (int k = 0; k < kShards; k++) s += h[slot * kShards + k];
-        out[i] = (int64_t)s;
-    }
-    return GOL_OK;
+    return run_read(c, [&]() -> int {
+        if (!(c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN))
+            return fail(c, GOL_ESTATE, "engine created without GOL_FLAG_COUNT_EVERY_TURN");
+        if (n == 0) return GOL_OK;
+        if (first_turn < 1 || first_turn + n - 1 > c->turn || first_turn <= c->turn - kRing)
+            return fail(c, GOL_EINVAL, "turns %lld..%lld not in the recorded window",
+                        (long long)first_turn, (long long)(first_turn + n - 1));
+        DeviceGuard g(c->device);
+        std::vector<unsigned long long> h((size_t)kRing * kShards);
+        HIP_OR_FAIL(c, hipMemcpyAsync(h.data(), c->counts, h.size() * 8, hipMemcpyDeviceToHost,
+                                      c->stream));
+        if (int rc = sync_checked(c)) return rc;
+        for (int64_t i = 0; i < n; ++i) {
+            const size_t slot = (size_t)((first_turn + i) % kRing);
+            unsigned long long s = 0;
+            for (int k = 0; k < kShards; k++) s += h[slot * kShards + k];
+            out[i] = (int64_t)s;
+        }
+        return GOL_OK;
+    });
 }
 
 int gol_read_board(gol_ctx *c, uint8_t *out)
 {
     if (!c || !out) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    const size_t row_bytes = (size_t)c->cfg.width;
-    if (!c->raw_turn0.empty()) {
-        std::memcpy(out, c->raw_turn0.data(), c->raw_turn0.size());
+    return run_read(c, [&]() -> int {
+        const size_t row_bytes = (size_t)c->cfg.width;
+        if (!c->raw_turn0.empty()) {
+            std::memcpy(out, c->raw_turn0.data(), c->raw_turn0.size());
+            return GOL_OK;
+        }
+        DeviceGuard g(c->device);
+        if (int rc_ = ensure_layout(c, false)) return rc_;
+        const int chunk_rows = (int)std::max<size_t>(
+            1, std::min<size_t>(kStagingBytes / row_bytes, (size_t)c->cfg.rows));
+        int rc = ensure_staging(c, (size_t)chunk_rows * row_bytes);
+        if (rc) return rc;
+        for (int r0 = 0; r0 < c->cfg.rows; r0 += chunk_rows) {
+            const int nr = std::min(chunk_rows, c->cfg.rows - r0);
+            HIP_OR_FAIL(c, golk::launch_unpack(c->board[c->cur], c->cfg.width, c->nw, c->pitch,
+                                               own_lo(c) + r0, nr, c->staging, c->stream));
+            HIP_OR_FAIL(c, hipMemcpyAsync(out + (size_t)r0 * row_bytes, c->staging,
+                                          (size_t)nr * row_bytes, hipMemcpyDeviceToHost, c->stream));
+            if (int rc2 = sync_checked(c)) return rc2;
+        }
         return GOL_OK;
-    }
-    DeviceGuard g(c->device);
-    if (int rc_ = ensure_layout(c, false)) return rc_;
-    const int chunk_rows = (int)std::max<size_t>(
-        1, std::min<size_t>(kStagingBytes / row_bytes, (size_t)c->cfg.rows));
-    int rc = ensure_staging(c, (size_t)chunk_rows * row_bytes);
-    if (rc) return rc;
-    for (int r0 = 0; r0 < c->cfg.rows; r0 += chunk_rows) {
-        const int nr = std::min(chunk_rows, c->cfg.rows - r0);
-        HIP_OR_FAIL(c, golk::launch_unpack(c->board[c->cur], c->cfg.width, c->nw, c->pitch,
-                                           own_lo(c) + r0, nr, c->staging, c->stream));
-        HIP_OR_FAIL(c, hipMemcpyAsync(out + (size_t)r0 * row_bytes, c->staging,
-                                      (size_t)nr * row_bytes, hipMemcpyDeviceToHost, c->stream));
-        HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
-    }
-    return GOL_OK;
+    });
 }
 
 int gol_read_packed(gol_ctx *c, uint64_t *out)
 {
     if (!c || !out) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    if (int rc_ = ensure_layout(c, false)) return rc_;
-    HIP_OR_FAIL(c, hipMemcpy2DAsync(out, (size_t)c->nw * 8,
-                                    c->board[c->cur] + (size_t)own_lo(c) * c->pitch,
-                                    (size_t)c->pitch * 8, (size_t)c->nw * 8, c->cfg.rows,
-                                    hipMemcpyDeviceToHost, c->stream));
-    HIP_OR_FAIL(c, hipStreamSynchronize(c->stream));
-    return GOL_OK;
+    return run_read(c, [&]() -> int {
+        DeviceGuard g(c->device);
+        if (int rc_ = ensure_layout(c, false)) return rc_;
+        HIP_OR_FAIL(c, hipMemcpy2DAsync(out, (size_t)c->nw * 8,
+                                        c->board[c->cur] + (size_t)own_lo(c) * c->pitch,
+                                        (size_t)c->pitch * 8, (size_t)c->nw * 8, c->cfg.rows,
+                                        hipMemcpyDeviceToHost, c->stream));
+        return sync_checked(c);
+    });
 }
 
 int gol_alive_cells(gol_ctx *c, int64_t *xy, int64_t cap, int64_t *n)
 {
     if (!c || !n || cap < 0 || (cap > 0 && !xy)) return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    if (int rc_ = ensure_layout(c, false)) return rc_;
-    const int rows = c->cfg.rows;
-    std::vector<long long> rc((size_t)rows), off((size_t)rows);
-    long long *d_rc = nullptr;
-    HIP_OR_FAIL(c, hipMalloc((void **)&d_rc, (size_t)rows * 8 * 2));
-    long long *d_off = d_rc + rows;
-    int err = GOL_OK;
-    auto done = [&](int code) {
-        (void)hipStreamSynchronize(c->stream);
-        (void)hipFree(d_rc);
-        return code;
-    };
-    hipError_t e = golk::launch_row_popcount(c->board[c->cur], c->nw, c->pitch, own_lo(c), rows,
-                                             d_rc, c->stream);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(rc.data(), d_rc, (size_t)rows * 8, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) return done(fail(c, GOL_EHIP, "alive count: %s", hipGetErrorString(e)));
-    long long total = 0;
-    for (int r = 0; r < rows; r++) {
-        off[(size_t)r] = total;
-        total += rc[(size_t)r];
-    }
-    *n = total;
-    if (cap == 0 || total == 0) return done(GOL_OK);
-    // scatter in row chunks so the device list stays within the staging budget
-    const long long per_cell = 16;
-    long long r0 = 0;
-    while (r0 < rows && off[(size_t)r0] < cap) {
-        // rows [r0, r1) whose cells fit in kStagingBytes
-        long long r1 = r0;
-        while (r1 < rows && (off[(size_t)r1] + rc[(size_t)r1] - off[(size_t)r0]) * per_cell <=
-                                (long long)kStagingBytes)
-            ++r1;
-        if (r1 == r0) r1 = r0 + 1;  // a single row larger than the budget
-        const long long cells = off[(size_t)r1 - 1] + rc[(size_t)r1 - 1] - off[(size_t)r0];
-        err = ensure_staging(c, (size_t)std::max<long long>(cells * per_cell, 16));
-        if (err) return done(err);
-        // offsets relative to this chunk: subtract off[r0] via a shifted copy
-        std::vector<long long> rel((size_t)(r1 - r0));
-        for (long long r = r0; r < r1; r++) rel[(size_t)(r - r0)] = off[(size_t)r] - off[(size_t)r0];
-        e = hipMemcpyAsync(d_off + r0, rel.data(), rel.size() * 8, hipMemcpyHostToDevice,
-                           c->stream);
+    return run_read(c, [&]() -> int {
+        DeviceGuard g(c->device);
+        if (int rc_ = ensure_layout(c, false)) return rc_;
+        const int rows = c->cfg.rows;
+        std::vector<long long> rc((size_t)rows), off((size_t)rows);
+        long long *d_rc = nullptr;
+        HIP_OR_FAIL(c, hipMalloc((void **)&d_rc, (size_t)rows * 8 * 2));
+        long long *d_off = d_rc + rows;
+        int err = GOL_OK;
+        auto done = [&](int code) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipFree(d_rc);
+            return code;
+        };
+        hipError_t e = golk::launch_row_popcount(c->board[c->cur], c->nw, c->pitch, own_lo(c), rows,
+                                                 d_rc, c->stream);
         if (e == hipSuccess)
-            e = golk::launch_alive_scatter(c->board[c->cur], c->nw, c->pitch,
-                                           own_lo(c) + (int)r0, (int)(r1 - r0),
-                                           (long long)c->cfg.row_offset + r0, d_off + r0,
-                                           (long long *)c->staging, c->stream);
-        const long long want = std::min<long long>(cells, cap - off[(size_t)r0]);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(xy + 2 * off[(size_t)r0], c->staging, (size_t)want * per_cell,
-                               hipMemcpyDeviceToHost, c->stream);
+            e = hipMemcpyAsync(rc.data(), d_rc, (size_t)rows * 8, hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess)
-            return done(fail(c, GOL_EHIP, "alive scatter: %s", hipGetErrorString(e)));
-        r0 = r1;
-    }
-    return done(GOL_OK);
+        if (e != hipSuccess) return done(fail(c, GOL_EHIP, "alive count: %s", hipGetErrorString(e)));
+        if (int rc2 = check_dev_err(c)) return done(rc2);
+        long long total = 0;
+        for (int r = 0; r < rows; r++) {
+            off[(size_t)r] = total;
+            total += rc[(size_t)r];
+        }
+        *n = total;
+        if (cap == 0 || total == 0) return done(GOL_OK);
+        // scatter in row chunks so the device list stays within the staging budget
+        const long long per_cell = 16;
+        long long r0 = 0;
+        while (r0 < rows && off[(size_t)r0] < cap) {
+            // rows [r0, r1) whose cells fit in kStagingBytes
+            long long r1 = r0;
+            while (r1 < rows && (off[(size_t)r1] + rc[(size_t)r1] - off[(size_t)r0]) * per_cell <=
+                                    (long long)kStagingBytes)
+                ++r1;
+            if (r1 == r0) r1 = r0 + 1;  // a single row larger than the budget
+            const long long cells = off[(size_t)r1 - 1] + rc[(size_t)r1 - 1] - off[(size_t)r0];
+            err = ensure_staging(c, (size_t)std::max<long long>(cells * per_cell, 16));
+            if (err) return done(err);
+            // offsets relative to this chunk: subtract off[r0] via a shifted copy
+            std::vector<long long> rel((size_t)(r1 - r0));
+            for (long long r = r0; r < r1; r++) rel[(size_t)(r - r0)] = off[(size_t)r] - off[(size_t)r0];
+            e = hipMemcpyAsync(d_off + r0, rel.data(), rel.size() * 8, hipMemcpyHostToDevice,
+                               c->stream);
+            if (e == hipSuccess)
+                e = golk::launch_alive_scatter(c->board[c->cur], c->nw, c->pitch,
+                                               own_lo(c) + (int)r0, (int)(r1 - r0),
+                                               (long long)c->cfg.row_offset + r0, d_off + r0,
+                                               (long long *)c->staging, c->stream);
+            const long long want = std::min<long long>(cells, cap - off[(size_t)r0]);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(xy + 2 * off[(size_t)r0], c->staging, (size_t)want * per_cell,
+                                   hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess)
+                return done(fail(c, GOL_EHIP, "alive scatter: %s", hipGetErrorString(e)));
+            r0 = r1;
+        }
+        return done(GOL_OK);
+    });
 }
 
 // ------------------------------------------------------------ halo exchange
@@ -1368,15 +1743,14 @@ static int copy_rows_between(gol_ctx *dst, int dst_row, gol_ctx *src, int src_ro
         DeviceGuard gs(src->device);
         if (int rc = ensure_layout(src, dst->il)) return rc;
     }
-    // dst stream waits for src's queued work; copy on dst's stream
-    hipEvent_t ev;
+    // dst stream waits for src's queued work (src's event, on src's device); copy on dst's
+    // stream; then src's stream waits for the copy (dst's event)
     {
         DeviceGuard g(src->device);
-        HIP_OR_FAIL(dst, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_OR_FAIL(dst, hipEventRecord(ev, src->stream));
+        HIP_OR_FAIL(dst, hipEventRecord(src->ev_copy, src->stream));
     }
     DeviceGuard g(dst->device);
-    HIP_OR_FAIL(dst, hipStreamWaitEvent(dst->stream, ev, 0));
+    HIP_OR_FAIL(dst, hipStreamWaitEvent(dst->stream, src->ev_copy, 0));
     const size_t rowb = (size_t)dst->nw * 8;
     uint64_t *d = dst->board[dst->cur] + (size_t)dst_row * dst->pitch;
     const uint64_t *s = src->board[src->cur] + (size_t)src_row * src->pitch;
@@ -1389,15 +1763,11 @@ static int copy_rows_between(gol_ctx *dst, int dst_row, gol_ctx *src, int src_ro
                                             dst->stream));
     }
     // src must not overwrite these rows before the copy lands
-    hipEvent_t back;
-    HIP_OR_FAIL(dst, hipEventCreateWithFlags(&back, hipEventDisableTiming));
-    HIP_OR_FAIL(dst, hipEventRecord(back, dst->stream));
+    HIP_OR_FAIL(dst, hipEventRecord(dst->ev_copy, dst->stream));
     {
         DeviceGuard g2(src->device);
-        HIP_OR_FAIL(dst, hipStreamWaitEvent(src->stream, back, 0));
+        HIP_OR_FAIL(dst, hipStreamWaitEvent(src->stream, dst->ev_copy, 0));
     }
-    (void)hipEventDestroy(back);
-    (void)hipEventDestroy(ev);
     return GOL_OK;
 }
 
@@ -1405,8 +1775,9 @@ int gol_copy_halo_from_upper(gol_ctx *dst, gol_ctx *src)
 {
     if (!dst || !src || !is_strip(dst) || !is_strip(src) || dst->cfg.halo != src->cfg.halo)
         return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> l1(dst->mu);
-    std::lock_guard<std::recursive_mutex> l2(src->mu);
+    // both engines at once, deadlock-free in any order (a ring pair exchanging both ways from
+    // two host threads); dst == src (one strip exchanging with itself) is one recursive lock
+    std::scoped_lock lk(dst->mu, src->mu);
     const int K = dst->cfg.halo;
     return copy_rows_between(dst, 0, src, own_hi(src) - K, K);
 }
@@ -1415,8 +1786,7 @@ int gol_copy_halo_from_lower(gol_ctx *dst, gol_ctx *src)
 {
     if (!dst || !src || !is_strip(dst) || !is_strip(src) || dst->cfg.halo != src->cfg.halo)
         return GOL_EINVAL;
-    std::lock_guard<std::recursive_mutex> l1(dst->mu);
-    std::lock_guard<std::recursive_mutex> l2(src->mu);
+    std::scoped_lock lk(dst->mu, src->mu);
     const int K = dst->cfg.halo;
     return copy_rows_between(dst, own_hi(dst), src, own_lo(src), K);
 }

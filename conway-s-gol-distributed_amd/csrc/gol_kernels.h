@@ -34,7 +34,19 @@ struct StepArgs {
     // k_step_wg wave priorities (4-wave workgroups): wave w runs at s_setprio
     // (wg_prio >> 2w) & 3; 0 = the built-in grading
     unsigned wg_prio;
+    // engine-owned error word (host-mapped pinned memory, or nullptr): a k_step_wg wait that
+    // gives up stores a kDevErr* code here, and the engine reports it as GOL_EHIP at its next
+    // synchronising call instead of returning a corrupt board with GOL_OK
+    unsigned *err;
+    // k_step_tile (kMultiTile): tile width in words (the tile height is `band`) and rows per
+    // lane segment
+    int tile_w;
+    int tile_seg;
 };
+
+// device error codes (StepArgs::err)
+constexpr unsigned kDevErrHandoff = 1u;    // k_step_wg: LDS hand-off wait timed out
+constexpr unsigned kDevErrPgFlag = 2u;     // k_step_wg parallelogram: flag wait timed out
 
 // temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkewILW16 is shipped)
 enum : int {
@@ -59,9 +71,25 @@ enum : int {
     kMultiWgHxS = 13,       // kMultiWgHx with each wave's stages in order within a step (fill
                             //   and drain of 2 instead of 3 steps per stage)
     kMultiWgPgS = 14,       // kMultiWgPg, stages in order (band rule: golk::pg_ok(.., true))
-    kMultiCount = 15,
+    kMultiTile = 15,        // k_step_tile: a 2-D tile per workgroup, resident in registers for
+                            //   all K turns (small boards: gol_tile.h)
+    kMultiCount = 16,
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
+
+#ifndef GOL_TOOLS
+#define GOL_TOOLS 0   // 1: the tools build (libgolamd_tools.so, see the Makefile)
+#endif
+
+// the kernels the product library ships (gol_create_ex rejects the others unless GOL_TOOLS):
+// k_step_skew on the interleaved layout with 16-B row DMA, the k_step_wg families and the
+// LDS tile kernel.  The superseded skew variants (kMultiSerial .. kMultiSkewIL), the timing
+// ablations and the wait diagnostics exist in the tools build only.
+constexpr bool multi_variant_shipped(int v)
+{
+    return v == kMultiSkewILW16 || v == kMultiWg || v == kMultiWgHx || v == kMultiWgPg ||
+           v == kMultiWgHxS || v == kMultiWgPgS || v == kMultiTile;
+}
 
 // the k_step_wg variants (one band pipeline per workgroup)
 constexpr bool is_wg_variant(int v)
@@ -151,6 +179,12 @@ int multi_blocks_per_cu(int turns, int words_per_lane, int variant);
 int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacity_waves,
                     int variant);
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
+// k_step_tile (gol_tile.hip): a launch of `turns` turns on tiles of band x tile_w words with
+// tile_seg rows per lane; shape check, workgroup waves, tile count
+bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg);
+int tile_waves(int turns, int tile_h, int tile_w, int seg);
+long long tile_count(int nw, int rows, int tile_h, int tile_w);
+hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);
 

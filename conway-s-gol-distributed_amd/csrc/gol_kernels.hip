@@ -618,7 +618,8 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
 
 int multi_max_turns(int variant)
 {
-    if (variant == kMultiWgHx || variant == kMultiWgPg) return kWgDeepMax;
+    if (variant == kMultiTile) return kMaxTurnsPerLaunch;
+    if (variant == kMultiWgHx || variant == kMultiWgPg) return GOL_TOOLS ? kWgDeepMax : 16;
     if (variant == kMultiWgHxS || variant == kMultiWgPgS) return 16;
     return is_wg_variant(variant) ? 16 : variant == kMultiSkewILW16 ? 12 : 8;
 }
@@ -731,6 +732,7 @@ static hipError_t launch_multi_v(const StepArgs &a, int turns, hipStream_t s)
 template <int V>
 static int multi_blocks_per_cu_v(int turns, int variant)
 {
+    if (variant == kMultiTile) return 1;                // shape-dependent: the engine plans it
     int blocks = 0;
     void *fn = is_wg_variant(variant) ? (V == 1 ? wg_kernel(turns, variant) : nullptr)
                                       : skew_kernel(V, turns, variant);
@@ -780,6 +782,8 @@ int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacit
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s)
 {
     if (a.row_hi <= a.row_lo) return hipSuccess;
+    if (a.multi_variant == kMultiTile) return launch_tile(a, turns, s);
+    if (!GOL_TOOLS && a.multi_words != 1) return hipErrorInvalidValue;   // tools build only
     return a.multi_words == 1 ? launch_multi_v<1>(a, turns, s) : launch_multi_v<2>(a, turns, s);
 }
 

@@ -402,7 +402,7 @@ struct Strips {
             const long long n = std::min<long long>(turns, hv);
             for (auto *e : eng) {
                 int rc = gol_step(e, n);
-                if (rc) return fail_from(e, rc);
+                if (rc < 0) return fail_from(e, rc);   // (strip engines have no control word)
             }
             turns -= n;
         }

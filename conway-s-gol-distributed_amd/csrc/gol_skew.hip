@@ -6,6 +6,7 @@
 
 namespace golk {
 
+#if GOL_TOOLS   // K1m: superseded by K1s, tools build only
 // ------------------------------------- K1m: K turns per launch (temporal blocking)
 // A wavefront owns a tile of 128 words (64 lanes x 2 words) whose first and last lane
 // are halo lanes: only lanes 1..62 (124 words) are stored, tiles advance by 124 words.
@@ -154,6 +155,8 @@ __global__ __launch_bounds__(256, MULTI_MIN_WAVES) void k_step_multi(const uint6
     if (r < r_end) step(std::integral_constant<int, P0>{}, Kc{}, r);
     if (r + 1 < r_end) step(std::integral_constant<int, (P0 + 1) % 3>{}, Kc{}, r + 1);
 }
+
+#endif  // GOL_TOOLS
 
 // ------------------------- K1s: K turns per launch, skewed stage pipeline (the default)
 // Same tiles, halo lanes and bit-sliced rule as k_step_multi; three changes:
@@ -413,6 +416,7 @@ __global__ __launch_bounds__(256, MINW) void k_step_skew(const uint64_t *__restr
 // (MINW 4 = at most 128 VGPRs: 4 waves per SIMD; only 2 dwords per lane at K < 8 fits
 // without spills -- K = 8 needs 132 VGPRs, and forcing 128 spilled and ran 17 % slower)
 template <int Var, int K, int ND> struct SkewCfg;
+#if GOL_TOOLS   // superseded k_step_skew variants (A/B history in DESIGN.md): tools build only
 template <int K, int ND> struct SkewCfg<kMultiSkew, K, ND> {
     static constexpr int PD = 8, MINW = (ND == 2 && K < 8) ? 4 : 1;
     static constexpr bool R7 = true;
@@ -439,6 +443,7 @@ template <int K, int ND> struct SkewCfg<kMultiSkewIL, K, ND> {
     static constexpr int PD = 8, MINW = 4;
     static constexpr bool R7 = true;
 };
+#endif  // GOL_TOOLS
 // K = 9..12 (deeper launches, fewer of them): 3 waves/SIMD up to K = 10, 2 beyond
 template <int K, int ND> struct SkewCfg<kMultiSkewILW16, K, ND> {
     static constexpr int PD = 8, MINW = K <= 8 ? 4 : (K <= 10 ? 3 : 2);
@@ -446,12 +451,6 @@ template <int K, int ND> struct SkewCfg<kMultiSkewILW16, K, ND> {
 };
 
 
-
-template <int ABL>
-static void *abl_fn()
-{
-    return reinterpret_cast<void *>(&k_step_skew<8, 2, 8, 4, true, true, true, ABL>);
-}
 
 template <int K, int ND, int Var>
 static void *skew_fn()
@@ -462,8 +461,34 @@ static void *skew_fn()
                      Var == kMultiSkewILW16>);
 }
 
-// kernel for (turns, words per lane, variant); experimental variants exist for V = 1 and
-// K in {6, 8} only (kMultiSkewD1: K in {4, 6, 8}) and fall back to kMultiSkew elsewhere
+// the shipped k_step_skew: interleaved layout, 16-B row DMA, one word per lane, K = 2..12
+static void *ilw16_fn(int turns)
+{
+    switch (turns) {
+    case 2: return skew_fn<2, 2, kMultiSkewILW16>();
+    case 3: return skew_fn<3, 2, kMultiSkewILW16>();
+    case 4: return skew_fn<4, 2, kMultiSkewILW16>();
+    case 5: return skew_fn<5, 2, kMultiSkewILW16>();
+    case 6: return skew_fn<6, 2, kMultiSkewILW16>();
+    case 7: return skew_fn<7, 2, kMultiSkewILW16>();
+    case 8: return skew_fn<8, 2, kMultiSkewILW16>();
+    case 9: return skew_fn<9, 2, kMultiSkewILW16>();
+    case 10: return skew_fn<10, 2, kMultiSkewILW16>();
+    case 11: return skew_fn<11, 2, kMultiSkewILW16>();
+    case 12: return skew_fn<12, 2, kMultiSkewILW16>();
+    default: return nullptr;
+    }
+}
+
+#if GOL_TOOLS
+template <int ABL>
+static void *abl_fn()
+{
+    return reinterpret_cast<void *>(&k_step_skew<8, 2, 8, 4, true, true, true, ABL>);
+}
+
+// tools build: every variant for (turns, words per lane); experimental variants exist for
+// V = 1 and K in {6, 8} only (kMultiSkewD1: K in {4, 6, 8}) and fall back to kMultiSkew
 template <int V>
 static void *multi_fn(int turns, int variant)
 {
@@ -479,7 +504,7 @@ static void *multi_fn(int turns, int variant)
         default: return nullptr;
         }
     }
-    if (V == 1 && turns == 8 && variant >= kMultiAblate) {   // timing ablations (tools only)
+    if (V == 1 && turns == 8 && variant >= kMultiAblate) {   // timing ablations
         switch (variant - kMultiAblate) {
         case 1: return abl_fn<1>();
         case 2: return abl_fn<2>();
@@ -489,22 +514,7 @@ static void *multi_fn(int turns, int variant)
         default: return nullptr;
         }
     }
-    if (V == 1 && variant == kMultiSkewILW16) {
-        switch (turns) {
-        case 2: return skew_fn<2, 2, kMultiSkewILW16>();
-        case 3: return skew_fn<3, 2, kMultiSkewILW16>();
-        case 4: return skew_fn<4, 2, kMultiSkewILW16>();
-        case 5: return skew_fn<5, 2, kMultiSkewILW16>();
-        case 6: return skew_fn<6, 2, kMultiSkewILW16>();
-        case 7: return skew_fn<7, 2, kMultiSkewILW16>();
-        case 8: return skew_fn<8, 2, kMultiSkewILW16>();
-        case 9: return skew_fn<9, 2, kMultiSkewILW16>();
-        case 10: return skew_fn<10, 2, kMultiSkewILW16>();
-        case 11: return skew_fn<11, 2, kMultiSkewILW16>();
-        case 12: return skew_fn<12, 2, kMultiSkewILW16>();
-        default: return nullptr;
-        }
-    }
+    if (V == 1 && variant == kMultiSkewILW16) return ilw16_fn(turns);
     if (V == 1 && variant == kMultiSkewIL) {
         switch (turns) {
         case 2: return skew_fn<2, 2, kMultiSkewIL>();
@@ -552,5 +562,11 @@ void *skew_kernel(int words_per_lane, int turns, int variant)
 {
     return words_per_lane == 1 ? multi_fn<1>(turns, variant) : multi_fn<2>(turns, variant);
 }
+#else
+void *skew_kernel(int words_per_lane, int turns, int variant)
+{
+    return words_per_lane == 1 && variant == kMultiSkewILW16 ? ilw16_fn(turns) : nullptr;
+}
+#endif  // GOL_TOOLS
 
 }  // namespace golk

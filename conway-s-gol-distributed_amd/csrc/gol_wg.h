@@ -45,9 +45,22 @@ struct WgSplit {
 constexpr int kWgPD = kWgDmaRows;                       // wave 0's rows in flight
 constexpr int kWgRQ = kWgPD + 1;                        // its LDS-DMA ring slots
 constexpr int kWgR = 6;                                 // hand-off ring slots per boundary
-// A wait gives up after this many polls (~2^22 x 64 cycles, >0.1 s): a broken hand-off then
-// ends the launch with a wrong board (caught by the parity tests) instead of hanging the GPU.
-constexpr int kWgSpinLimit = 1 << 22;
+// A wait gives up after this many polls (~2^22 x 64 cycles, >0.1 s) instead of hanging the
+// GPU, and records that in the engine's error word (StepArgs::err): the engine then fails its
+// next synchronising call with GOL_EHIP rather than hand back the wrong board it computed.
+// (GOL_WG_SPIN_LIMIT: the test build libgolamd_spin0.so sets 0, so every wait gives up.)
+#ifndef GOL_WG_SPIN_LIMIT
+#define GOL_WG_SPIN_LIMIT (1 << 22)
+#endif
+constexpr int kWgSpinLimit = GOL_WG_SPIN_LIMIT;
+
+// a wait gave up: one store of the code from lane 0 into host-mapped memory (system scope,
+// so the host sees it after the launch completes; a plain store, no PCIe atomics needed)
+__device__ __forceinline__ void wg_report(unsigned *err, unsigned code)
+{
+    if (err && (threadIdx.x & 63) == 0)
+        __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // SYNC 2: consumer's initial lag (rows).  Each wave boundary adds it to the pipeline fill;
 // 1 measured as fast as 3 or slightly faster (16384^2 K = 16: 3.25 vs 3.27-3.33 us/turn; the
 // 8-strip shape 5.62 vs 5.66-5.95; 65536^2 equal)
@@ -235,6 +248,8 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     }
     uint32_t avail = 0;                                  // consumer: rows known to be written
     uint32_t room = R;                                   // producer: rows it may write
+    unsigned gave_up = 0;                                // kDevErr* of a wait that gave up
+                                                         //   (wave-uniform: reported at the end)
     constexpr bool DIAG = SYNC == 3;
     const unsigned long long d_r0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned long long d_t0 = DIAG ? __builtin_amdgcn_s_memtime() : 0, d_fw = 0, d_ew = 0,
@@ -262,6 +277,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
                     avail = lds_load_counter(&sh.produced[W - 1]);
                     if (avail < need) __builtin_amdgcn_s_sleep(1);
                 }
+                if (avail < need) gave_up = kDevErrHandoff;
                 if (DIAG && tw) {
                     const unsigned long long dt = __builtin_amdgcn_s_memtime() - tw;
                     if (q == 0) d_first += dt;
@@ -293,6 +309,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
                 room = lds_load_counter(&sh.consumed[W]) + R;
                 if (room <= (uint32_t)q) __builtin_amdgcn_s_sleep(1);
             }
+            if (room <= (uint32_t)q) gave_up = kDevErrHandoff;
             if (DIAG && tw) {
                 d_ew += __builtin_amdgcn_s_memtime() - tw;
                 ++d_ne;
@@ -367,11 +384,18 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
     // once per wave, after its last publication store (stage G-1's e = 1, step 3G): the flags
     auto publish_flags = [&]() {
         if constexpr (PG && NS > 0) {
+            // Ordering without cache maintenance: rows and flags live in uncached memory, so
+            // a row store is visible to every XCD once it has completed.  The wait completes
+            // the row stores before a flag store issues; the flag store's release order (at
+            // workgroup scope: no L2 write-back -- an agent-scope release would write back the
+            // XCD's whole L2, which holds this launch's board output) keeps the compiler from
+            // moving a row store below it.  (Compiler-only fences around the wait cost K <= 12
+            // one VGPR: 65 > 64, one wave per SIMD less.)
             __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // the stores are done
             if (lane == 0)
                 for (int jl = 0; jl < NS; ++jl)
                     __hip_atomic_store(&a.xflags[tx * kPgStages + J + jl], a.epoch,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     };
     // stage jl's 2 rows from below into LDS slot jl % 2 (16-B DMA from lanes 0..31)
@@ -393,13 +417,18 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
             for (int jl = 0; jl < NS; ++jl)
                 for (int t = t_a; t <= t_b; ++t) {
                     unsigned *f = &a.xflags[t * kPgStages + J + jl];
-                    for (int spin = 0; spin < kWgSpinLimit; ++spin) {
+                    bool seen = false;
+                    for (int spin = 0; !seen && spin < kWgSpinLimit; ++spin) {
                         const unsigned v = (unsigned)__builtin_amdgcn_readfirstlane((int)
                             __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                        if (v == a.epoch) break;
-                        __builtin_amdgcn_s_sleep(1);
+                        seen = v == a.epoch;
+                        if (!seen) __builtin_amdgcn_s_sleep(1);
                     }
+                    if (!seen) gave_up = kDevErrPgFlag;
                 }
+            // the row loads stay below the flag checks (the loop exits on the loaded value, so
+            // the hardware issues them after the flags arrived)
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
             for (int jl = 0; jl < NS && jl < 2; ++jl) nb_load(jl);
             __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // rows landed
         }
@@ -569,6 +598,7 @@ __device__ __forceinline__ void wg_wave(const uint64_t *__restrict__ in, uint64_
         }
     }
     if constexpr (FIRST) __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // DMAs landed
+    if (gave_up) wg_report(a.err, gave_up);
     if constexpr (DIAG) {
         if (lane == 0 && a.counts) {
             unsigned long long *d = a.counts + ((size_t)blockIdx.x * NW + W) * 10;

@@ -26,12 +26,17 @@ static void *wg_fn_nw(int turns)
 
 // kMultiWg: 4 waves per band, capped where that costs no spills: 64 VGPRs (8 waves per
 // SIMD) at K <= 12 (60 uncapped), 72 (7 waves) at K >= 13 (75 uncapped; 64 spills 28 B);
-// kMultiWgNoBar / kMultiWgDiag: timing ablation / wait diagnostics (tools only)
+// kMultiWgNoBar / kMultiWgDiag: timing ablation / wait diagnostics (GOL_TOOLS build only)
 static void *wg_fn(int turns, int variant)
 {
     switch (variant) {
+#if GOL_TOOLS
     case kMultiWgNoBar: return turns == 8 || turns == 16 ? wg_fn_nw<4, 0>(turns) : nullptr;
     case kMultiWgDiag: return turns == 8 || turns == 16 ? wg_fn_nw<4, 3>(turns) : nullptr;
+#else
+    case kMultiWgNoBar:
+    case kMultiWgDiag: return nullptr;                  // wrong-result builds: tools only
+#endif
     case kMultiWgHx: return wg_hx_kernel(turns, false);
     case kMultiWgPg: return wg_hx_kernel(turns, true);
     case kMultiWgHxS: return wg_ser_kernel(turns, false);

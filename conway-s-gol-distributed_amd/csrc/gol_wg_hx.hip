@@ -26,10 +26,15 @@ static void *wg_hx_fn(int turns)
 }
 
 // the register caps of kMultiWg: 8 waves per SIMD at K <= 12 (64 VGPRs), 7 at K >= 13 (72);
-// K > 16: helix only (launch_wg runs kMultiWgPg as kMultiWgHx there), wg_waves(K) waves
+// K > 16 (tools build): helix only (launch_wg runs kMultiWgPg as kMultiWgHx there), wg_waves(K)
+// waves
 void *wg_hx_kernel(int turns, bool pg)
 {
+#if GOL_TOOLS   // depths 17..32 measured slower per turn than 16: tools build only
     if (turns > 16) return pg ? nullptr : turns <= 24 ? wg_deep_kernel_a(turns) : wg_deep_kernel_b(turns);
+#else
+    if (turns > 16) return nullptr;
+#endif
     if (pg) return turns >= 13 ? wg_hx_fn<7, true>(turns) : wg_hx_fn<8, true>(turns);
     return turns >= 13 ? wg_hx_fn<7, false>(turns) : wg_hx_fn<8, false>(turns);
 }

@@ -29,10 +29,19 @@
  *     (:107-152, Server/gol/distributor.go:136-164) and the PGM I/O goroutine
  *     (Local/gol/io.go:42-143).
  *
- * Threading: an engine is driven by one thread at a time (every call takes the
- * engine's lock, as the reference Server's mutex serialises GetWorld/Alivecount
- * with the commit: Server/gol/distributor.go:63-73,131-134).  A run driver owns
- * its engines on its own thread; gol_run_* calls are thread-safe.
+ * Threading: one thread drives an engine (gol_step, loads, halo calls).  The read-only
+ * calls (gol_snapshot, gol_get_info, gol_read_board, gol_read_packed, gol_alive_cells,
+ * gol_turn_counts) may come from other threads at any time: during a gol_step the stepping
+ * thread serves them at its next launch boundary, on a turn-consistent board; while the
+ * step is parked on GOL_CONTROL_PAUSE they run at once (the reference Server's mutex is
+ * held only around the per-turn commit: Server/gol/distributor.go:62-75,131-134).  A run
+ * driver owns its engines on its own thread; gol_run_* calls are thread-safe.
+ *
+ * Return codes: GOL_OK or a negative GOL_E* code; gol_step returns GOL_STOPPED (> 0) when
+ * the control word stopped it, gol_last_launches a count.  Test failures with rc < 0.
+ * GOL_EHIP also reports a corrupt board: a k_step_wg pipeline wait that gave up (a starved
+ * workgroup) sets the engine's device error word, and every synchronising call fails until
+ * the board is replaced (gol_load*, gol_fill_random).
  */
 #ifndef GOL_AMD_H
 #define GOL_AMD_H

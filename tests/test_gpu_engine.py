@@ -16,8 +16,14 @@ import numpy as np
 import pytest
 
 import golden_data as G
+from conftest import tools_only
 
 pytestmark = pytest.mark.gpu
+
+
+def _tools(*vals):
+    """Parameters that exist in the tools build only (superseded kernels, see conftest)."""
+    return [pytest.param(v, marks=tools_only) for v in vals]
 
 SIZES = (16, 64, 512)
 
@@ -132,7 +138,7 @@ def test_stencil_variants(gol, oracle, monkeypatch, variant, w, h, band):
     assert counts.tolist() == wc.astype(np.int64).tolist()
 
 
-@pytest.mark.parametrize("mw", [1, 2])
+@pytest.mark.parametrize("mw", [1] + _tools(2))
 @pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 17), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (1024, 1, 5, 8), (512, 130, 1000, 24)])
@@ -150,7 +156,7 @@ def test_temporal_blocking(gol, oracle, monkeypatch, mw, tpl, w, h, band, turns)
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("mv", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("mv", [7] + _tools(0, 1, 2, 3, 4, 5, 6))
 @pytest.mark.parametrize("tpl", [6, 8])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 17), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (512, 130, 1000, 24),
@@ -204,6 +210,7 @@ def test_temporal_blocking_workgroup(gol, oracle, monkeypatch, mv, tpl, w, h, ba
     assert np.array_equal(got, oracle.bit_run(want_mid, w, turns + 3))
 
 
+@tools_only
 @pytest.mark.parametrize("mv", [9, 12])
 @pytest.mark.parametrize("tpl", [17, 18, 20, 21, 23, 24, 25, 28, 31, 32])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 40), (384, 3, 8, 35), (8320, 41, 7, 33),
@@ -285,7 +292,7 @@ def test_il_layout_roundtrip():
         assert not np.array_equal(il_layout(w, nd), w)
 
 
-@pytest.mark.parametrize("mv", [6, 7])
+@pytest.mark.parametrize("mv", [7] + _tools(6))
 @pytest.mark.parametrize("tpl", [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("w,h,band,turns", [(256, 64, 16, 19), (384, 3, 8, 11), (8320, 41, 7, 13),
                                             (16384, 70, 64, 9), (2048, 300, 137, 17),
@@ -314,7 +321,7 @@ def test_interleaved_raw_layout(gol, oracle, monkeypatch):
     """What the IL kernel computes on: a board whose words are il_layout() of the logical
     board.  Checked through a strip engine's halo export (standard rows) and the engine's
     own conversion, against the numpy restatement of the layout."""
-    monkeypatch.setenv("GOL_MULTI_VARIANT", "6")
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "7")
     torch = pytest.importorskip("torch")
     w, rows, K = 512, 40, 8
     start = oracle.gen_random(5, w, rows + 2 * K)
@@ -598,3 +605,173 @@ def test_control_word_pause_and_stop(gol, oracle):
     want = oracle.bit_run(oracle.gen_random(21, w, h), w, t_paused)
     assert np.array_equal(got, want)
     assert np.array_equal(after, oracle.bit_run(want, w, 7))
+
+
+# ------------------------------------------------------------- K1t k_step_tile
+TILE_CASES = [
+    # (width, height, tile_w, tile_h, seg, K, turns)
+    (5120, 5120, 10, 160, 4, 32, 70),     # BASELINE configs[1]'s shape: 8 x 32 tiles
+    (5120, 300, 10, 37, 3, 16, 40),       # short last tile row (300 = 8 x 37 + 4)
+    (1024, 203, 14, 20, 2, 8, 19),        # 16 words: a partial last tile column (2 words)
+    (384, 100, 6, 25, 6, 12, 25),         # nw = 6: one tile column, halo words wrap
+    (256, 40, 4, 40, 8, 32, 65),          # K > height / 2: the tile wraps the torus twice
+    (256, 3, 2, 1, 2, 24, 30),            # 1-row tiles on a 3-row torus
+    (8320, 41, 62, 13, 4, 20, 44),        # 64-lane groups (G = 1), ragged everything
+    (2048, 500, 30, 64, 8, 24, 50),       # G = 2
+    (4096, 257, 5, 50, 3, 10, 33),        # C = 7: 9 groups, 1 idle lane
+]
+
+
+@pytest.mark.parametrize("w,h,tw,th,seg,K,turns", TILE_CASES)
+def test_tile_kernel(gol, oracle, monkeypatch, w, h, tw, th, seg, K, turns):
+    """k_step_tile (K turns on a register-resident 2-D tile: K halo rows, one halo word each
+    side, row segments exchanged through LDS once per turn) is bit-exact for partial tiles,
+    tiles taller than the torus, every lane grouping and turn counts leaving shallower
+    launches; read mid-run and stepped on."""
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+    monkeypatch.setenv("GOL_TILE", f"{tw},{seg}")
+    start = oracle.gen_random(w + 3 * h + K, w, h)
+    with _engine(gol, w, h, band_rows=th, turns_per_launch=K) as e:
+        info = e.info()
+        assert info.turns_per_launch == K and info.band_rows == th
+        e.load_packed(start)
+        e.step(turns)
+        mid = e.read_packed()
+        e.step(turns + 1)
+        got = e.read_packed()
+        assert all(v == 15 for _, v, _ in e.last_launches())
+    want_mid = oracle.bit_run(start, w, turns)
+    assert np.array_equal(mid, want_mid)
+    assert np.array_equal(got, oracle.bit_run(want_mid, w, turns + 1))
+
+
+@pytest.mark.parametrize("w,h", [(5120, 5120), (2048, 2048), (512, 512), (1024, 96)])
+def test_small_board_default_is_tile(gol, oracle, w, h):
+    """Boards below 2^20 words autotune k_step_tile shapes (no flags): the engine picks one,
+    plans launches of >= 2 turns with it, and stays bit-exact."""
+    start = oracle.gen_random(w + h, w, h)
+    with _engine(gol, w, h) as e:
+        e.load_packed(start)
+        e.step(45)
+        plan = e.last_launches()
+        assert plan and all(v == 15 and k >= 2 for k, v, _ in plan), plan
+        got = e.read_packed()
+    assert np.array_equal(got, oracle.bit_run(start, w, 45))
+
+
+# ------------------------------------------------------- product / tools split
+@pytest.mark.parametrize("mv", [0, 1, 2, 3, 4, 5, 6, 10, 11, 101, 104])
+def test_product_rejects_tools_kernels(gol, monkeypatch, mv):
+    """The product library refuses the superseded variants, the no-sync timing ablation and
+    the wait diagnostics (they compute wrong boards or print diagnostics)."""
+    if os.environ.get("GOL_AMD_LIB", "").endswith("_tools.so"):
+        pytest.skip("tools build accepts them")
+    monkeypatch.setenv("GOL_MULTI_VARIANT", str(mv))
+    from gol import _native as N
+    with pytest.raises(N.GolError) as ei:
+        _engine(gol, 1024, 64, band_rows=16, turns_per_launch=8)
+    assert ei.value.code == -1
+
+
+def test_spin_timeout_reports_error():
+    """libgolamd_spin0.so (make spin0: every k_step_wg wait gives up at once) computes a wrong
+    board, and the engine says so: the device error word turns the next synchronising call
+    into GOL_EHIP instead of GOL_OK with a corrupt board.  Runs in a child process (the test
+    library is a second copy of the engine)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "conway-s-gol-distributed_amd", "build", "libgolamd_spin0.so")
+    assert os.path.exists(lib), "build it: make -C conway-s-gol-distributed_amd/csrc spin0"
+    code = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import gol
+from gol import _native as N
+e = gol.Engine(2048, 512, device=0, band_rows=43, turns_per_launch=16)
+e.fill_random(4)
+rc = N.lib().gol_step(e.handle, 16)
+assert rc == 0, rc
+try:
+    e.sync()
+except N.GolError as err:
+    print("EHIP" if err.code == N.GOL_EHIP else "OTHER", str(err))
+    try:
+        e.snapshot()
+    except N.GolError as err2:
+        print("STICKY", err2.code)
+    e.fill_random(4)
+    e.sync()
+    print("CLEARED")
+else:
+    print("NOERROR")
+"""
+    env = dict(os.environ, GOL_AMD_LIB=lib, GOL_MULTI_VARIANT="12")
+    r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "conway-s-gol-distributed_amd")],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout
+    assert "EHIP" in out and "timed out" in out, out
+    assert "STICKY -2" in out and "CLEARED" in out, out
+
+
+# ------------------------------------------------ concurrent reads while stepping
+def test_snapshot_while_stepping_and_paused(gol, oracle):
+    """gol_snapshot / gol_read_packed / gol_get_info from a second thread while gol_step runs
+    and while it is parked on PAUSE (the reference serves Alivecount / GetWorld at any time,
+    its mutex held only around the commit: Server/gol/distributor.go:62-75,131-134; the
+    ticker keeps firing while paused, Local/gol/distributor.go:117-130,154-167).  Each call
+    returns within a few launches with a (turn, alive) pair equal to the oracle's at that
+    turn, and the step runs on to the turn asked for."""
+    import threading
+    import time
+    from gol import _native as N
+    w = h = 256                                   # k_step_tile, a few us per launch: with
+    start = oracle.gen_random(31, w, h)           # the control word armed (2 launches queued)
+    total = 10 ** 9                               # (stopped below)
+    with _engine(gol, w, h) as e:
+        e.load_packed(start)
+        e.set_control(N.GOL_CONTROL_RUN)
+        res = {}
+        th = threading.Thread(target=lambda: res.update(done=e.step(total)), daemon=True)
+        th.start()
+        seen = []
+        for _ in range(5):
+            t0 = time.time()
+            seen.append(e.snapshot())
+            assert time.time() - t0 < 2.0
+            time.sleep(0.002)
+        board_t = None
+        e.set_control(N.GOL_CONTROL_PAUSE)
+        t_end = time.time() + 10
+        while not e.progress()[1] and time.time() < t_end:
+            time.sleep(0.001)
+        t_paused, parked = e.progress()
+        assert parked
+        t0 = time.time()
+        snap_p = e.snapshot()
+        board_p = e.read_packed()
+        info_p = e.info()
+        assert time.time() - t0 < 2.0
+        assert snap_p[0] == t_paused and info_p.turn == t_paused
+        assert e.progress() == (t_paused, True)
+        e.set_control(N.GOL_CONTROL_RUN)          # runs on from the paused turn
+        time.sleep(0.02)
+        e.set_control(N.GOL_CONTROL_STOP)
+        th.join(60)
+        assert not th.is_alive() and res["done"] is False
+        total = e.turn
+        assert total > t_paused
+        final = e.read_packed()
+    # every snapshot is the oracle's count at its turn; the paused board is the oracle's
+    turns = sorted({t for t, _ in seen} | {t_paused})
+    board, at, counts = start, 0, {}
+    for t in turns:
+        board = oracle.bit_run(board, w, t - at)
+        at = t
+        counts[t] = oracle.popcount(board, w)
+        if t == t_paused:
+            assert np.array_equal(board_p, board)
+    for t, a in seen + [snap_p]:
+        assert a == counts[t], (t, a)
+    assert np.array_equal(final, oracle.bit_run(board, w, total - at))

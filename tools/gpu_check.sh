@@ -40,6 +40,11 @@ for step in "$@"; do
     strips78) run strips78 400 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --tpl 0,7,8 --rccl direct ;;
     calib)  run calib 300 bash tools/calib/run.sh ;;
     sweep)  run sweep 400 python -u tools/sweep.py --variants 2,4,5,6 --bands 16,32,64,128,256 ;;
+    c2def)  run c2def 300 python -u bench.py --size 5120 --steps 1000 --warmup 40 --c3-size 0 --no-cpu-baseline ;;
+    c2sweep) run c2sweep 500 python -u tools/sweep.py --size 5120 --variants 2 --bands 16,24,32,48,64 --tpl 4,8,12,16 --mw 1 --mv 7,9,12 --turns 960 ;;
+    sq65)   run sq65 300 bash tools/pmc_sq.sh ;;
+    newt)   run newt 400 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "tile or small_board or rejects_tools or spin_timeout or snapshot_while or control_word or 5120 or random_vs_oracle" ;;
+    c2tile) run c2tile 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --shapes 10:160:4:32,10:160:4:16,10:160:3:24,10:160:8:32,10:80:4:16,10:80:2:12,16:160:4:24,14:160:4:24,20:320:4:32,40:320:8:32 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done
