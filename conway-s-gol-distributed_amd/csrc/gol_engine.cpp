@@ -451,32 +451,40 @@ struct TileShape {
     double model_us = 0;                     // modelled time per turn
 };
 
-// Modelled time per turn of k_step_tile at one shape: per turn a wave
-// issues (SEG + 2) row sums (2 DPP + 2 v_alignbit at 4 cycles, 4 v_bitop3 at 2: 24 cycles)
-// and SEG rules (14 v_bitop3: 28 cycles); a SIMD issues its resident waves' work back to back
-// but one wave alone runs ~2.5x slower than issue (dependent VALU latency, calibrated by
-// tools/calib/valu_issue.hip); each turn adds a barrier, each launch its tile load and a
-// launch gap.
+// Modelled time per turn of k_step_tile at one shape, fitted to the
+// measured shapes of profiles/r03_tile_*.log: a wave issues (SEG + 2) row sums (8 VALU) and
+// SEG rules (14 VALU) per turn, at ~2.36 SIMD cycles per instruction (18 full-rate v_bitop3,
+// 4 half-rate v_alignbit / DPP moves per row pair); a SIMD shares its issue between its
+// resident waves, one wave alone issues at most every ~5 cycles, and each turn adds a barrier
+// and the LDS exchange -- cheaper to hide with >= 2 workgroups per CU (~80 % of the issue
+// rate and ~700 cycles a turn) than with one (~70 %, ~900).  A workgroup of `seg` rows per
+// lane holds ~2 seg + 30 VGPRs.
 double tile_model_us(int ncu, int nw, int rows, int K, int th, int tw, int seg)
 {
     if (!golk::tile_shape_ok(nw, K, th, tw, seg)) return 0;
     const long long tiles = golk::tile_count(nw, rows, th, tw);
     const int waves = golk::tile_waves(K, th, tw, seg);
-    const int wgpc = std::max(1, std::min(32 / waves, 4));            // waves / CU, LDS
+    const int vgpr = (2 * seg + 30 + 7) / 8 * 8;
+    const int wps_max = std::min(8, 512 / vgpr);                      // waves per SIMD
+    const int wgpc = std::max(1, std::min(4 * wps_max / waves, 5));    // (32 KB LDS each)
     const long long slots = (long long)ncu * wgpc;
     const long long rounds = (tiles + slots - 1) / slots;
     const long long per_cu = std::min<long long>((tiles + ncu - 1) / ncu, wgpc);
-    const double wps = (double)(per_cu * waves) / 4.0;                 // waves per SIMD
-    const double cyc_wave = (seg + 2) * 24.0 + seg * 28.0;
-    const double turn_cyc = std::max(std::ceil(wps), 2.5) * cyc_wave + 150.0;
+    const double instr = (seg + 2) * 8.0 + seg * 14.0;                 // per wave and turn
+    const double issue = (double)(per_cu * waves) * instr * 2.36 / 4.0;
+    const bool two = per_cu >= 2;
+    const double turn_cyc = std::max(issue / (two ? 0.8 : 0.7), instr * 5.0) + (two ? 700 : 900);
     const double launch_us = rounds * (K * turn_cyc + 2500.0) / 2400.0 + 3.0;
     return launch_us / K;
 }
 
-// The shapes the model ranks best for a board of nw words x rows (one per (K, TW), best TH
-// and SEG), fastest first.
+// The shapes the model ranks best for a board of nw words x rows (the best TH and SEG per
+// (K, TW)), fastest first.  TW: every width that splits a row into ntx near-equal tiles; TH:
+// the tallest tile the workgroup holds (16 waves) and the heights whose tile count fills 1..4
+// resident tiles per CU or a few more tile rows.
 std::vector<TileShape> tile_candidates(int ncu, int nw, int rows, int keep)
 {
+    static const int kSegs[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48};
     std::vector<TileShape> all;
     std::vector<int> tws;
     for (int ntx = 1; ntx <= nw; ++ntx) {
@@ -486,11 +494,18 @@ std::vector<TileShape> tile_candidates(int ncu, int nw, int rows, int keep)
     for (int K : {8, 12, 16, 20, 24, 32}) {
         for (int tw : tws) {
             TileShape best;
+            const int C = tw + 2, G = 64 / C;
             const long long ntx = (nw + tw - 1) / tw;
-            for (int per_cu : {1, 2, 3, 4}) {
-                const long long nty = std::max<long long>(1, ((long long)ncu * per_cu + ntx - 1) / ntx);
-                const int th = (int)std::max<long long>(1, (rows + nty - 1) / nty);
-                for (int seg : {2, 3, 4, 6, 8}) {
+            for (int seg : kSegs) {
+                const int thmax = golk::kTileMaxWavesHost * G * seg - 2 * K;
+                if (thmax < 1) continue;
+                std::vector<long long> ntys;
+                const long long nty0 = (rows + thmax - 1) / thmax;
+                for (long long n = nty0; n < nty0 + 4; ++n) ntys.push_back(n);
+                for (int per_cu = 1; per_cu <= 4; ++per_cu)
+                    ntys.push_back(std::max(nty0, ((long long)ncu * per_cu + ntx - 1) / ntx));
+                for (long long nty : ntys) {
+                    const int th = (int)std::max<long long>(1, (rows + nty - 1) / nty);
                     const double m = tile_model_us(ncu, nw, rows, K, th, tw, seg);
                     if (m > 0 && (best.K == 0 || m < best.model_us)) best = {K, th, tw, seg, m};
                 }
@@ -500,8 +515,18 @@ std::vector<TileShape> tile_candidates(int ncu, int nw, int rows, int keep)
     }
     std::sort(all.begin(), all.end(),
               [](const TileShape &x, const TileShape &y) { return x.model_us < y.model_us; });
-    if ((int)all.size() > keep) all.resize((size_t)keep);
-    return all;
+    // the model ranks, the autotune decides: keep the list diverse (at most 2 depths per tile
+    // width among the first picks)
+    std::vector<TileShape> out;
+    std::map<int, int> per_tw;
+    for (const TileShape &t : all)
+        if (per_tw[t.tw]++ < 2 && (int)out.size() < keep) out.push_back(t);
+    for (const TileShape &t : all)
+        if ((int)out.size() < keep && per_tw[t.tw] > 2) {
+            out.push_back(t);
+            per_tw[t.tw] = 0;               // (each width once more at most)
+        }
+    return out;
 }
 
 void apply_tile(gol_ctx *c, const TileShape &t)
@@ -519,7 +544,7 @@ void apply_tile(gol_ctx *c, const TileShape &t)
 // model's best k_step_tile shapes on the engine's own buffers and keep the fastest.
 void autotune_small(gol_ctx *c)
 {
-    std::vector<TileShape> cand = tile_candidates(c->ncu, c->nw, c->buf_rows, 24);
+    std::vector<TileShape> cand = tile_candidates(c->ncu, c->nw, c->buf_rows, 20);
     if (cand.empty()) return;
     golk::StepArgs a{};
     a.width = c->cfg.width;
@@ -590,14 +615,25 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     std::vector<int> vars{c->multi_variant};
     if (tune_variant)
         vars = {golk::kMultiSkewILW16, golk::kMultiWg, golk::kMultiWgHx, golk::kMultiWgPg,
-                golk::kMultiWgHxS, golk::kMultiWgPgS};
+                golk::kMultiWgHxS, golk::kMultiWgPgS, golk::kMultiTile};
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
     struct Cand {
         int var, K, band;
+        int tw = 0, seg = 0;                         // k_step_tile shape
     };
     std::vector<Cand> cand;
     for (int var : vars) {
+        if (var == golk::kMultiTile) {
+            // the model's best tile shapes (their own K and height), timed like the rest
+            int kept = 0;
+            for (const TileShape &ts : tile_candidates(ncu, c->nw, c->buf_rows, 64)) {
+                if (!tune_k && ts.K != c->tpl) continue;
+                cand.push_back({var, ts.K, ts.th, ts.tw, ts.seg});
+                if (++kept == 10) break;
+            }
+            continue;
+        }
         // K = 7 measured no faster than 6 / 8 on k_step_skew (DESIGN); k_step_wg goes to 16
         std::vector<int> ks = !golk::is_wg_variant(var) ? std::vector<int>{6, 8, 10}
                                                   : std::vector<int>{8, 12, 16};
@@ -657,6 +693,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     auto time_one = [&](const Cand &cd, int reps) -> float {
         a.band = cd.band;
         a.multi_variant = cd.var;
+        a.tile_w = cd.tw;
+        a.tile_seg = cd.seg;
         bool ok = hipEventRecord(e0, c->stream) == hipSuccess;
         for (int rep = 0; rep < reps && ok; ++rep) {
             a.in = c->board[rep & 1];
@@ -701,7 +739,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                 if (cand[i].var == var && cand[i].K == cand[j].K && t[i] > 0.f &&
                     (bi < 0 || t[i] < t[bi]))
                     bi = (int)i;
-            if (bi != (int)j) continue;
+            if (bi != (int)j || var == golk::kMultiTile) continue;
             const Cand b = cand[bi];
             const int step = golk::is_pg_variant(var) ? golk::kWgU : std::max(2, b.band / 16);
             for (int d : {-2, -1, 1, 2}) {
@@ -713,7 +751,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                 for (const Cand &x : cand)
                     seen |= x.var == var && x.K == b.K && x.band == band;
                 if (!seen) {
-                    cand.push_back({var, b.K, band});
+                    cand.push_back({var, b.K, band, 0, 0});
                     t.push_back(0.f);
                 }
             }
@@ -725,13 +763,13 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
         if (t[i] > 0.f && (best == 0.f || t[i] < best)) best = t[i];
     if (getenv("GOL_AUTOTUNE_LOG"))   // tools only: the measured table on stderr
         for (size_t i = 0; i < cand.size(); ++i)
-            fprintf(stderr, "autotune %dx%d var=%d K=%d band=%d us_per_turn=%.3f reps=%d\n",
-                    c->cfg.width, c->buf_rows, cand[i].var, cand[i].K, cand[i].band,
-                    t[i] * 1000.f, reps);
+            fprintf(stderr, "autotune %dx%d var=%d K=%d band=%d tile=%d,%d us_per_turn=%.3f "
+                    "reps=%d\n", c->cfg.width, c->buf_rows, cand[i].var, cand[i].K, cand[i].band,
+                    cand[i].tw, cand[i].seg, t[i] * 1000.f, reps);
     // within 1.5 % of the best, the deepest K wins: the same steady rate with fewer launches
     // when a run is short (65536^2, 20 turns: K = 10 -> 2 launches, 104.7k GCUPS; K = 8 ->
     // 7 + 7 + 6, 100.8k; steady state 36.0 vs 36.2 us/turn)
-    Cand pick{c->multi_variant, c->tpl, c->band_multi};
+    Cand pick{c->multi_variant, c->tpl, c->band_multi, c->tile_w, c->tile_seg};
     float pick_t = 0.f;
     for (size_t i = 0; i < cand.size(); ++i) {
         if (t[i] <= 0.f || t[i] > best * 1.015f) continue;
@@ -749,7 +787,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     std::vector<Launch> plan;
     if (tune_k && tune_variant && pick_t > 0.f) {
         struct Fam {
-            int var, K, band;
+            int var, K, band, tw, seg;
             float T[golk::kMaxTurnsPerLaunch + 1];
             int band_k[golk::kMaxTurnsPerLaunch + 1];
         };
@@ -759,7 +797,11 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             for (size_t i = 0; i < cand.size(); ++i)
                 if (cand[i].var == var && t[i] > 0.f && (bi < 0 || t[i] < t[bi])) bi = (int)i;
             if (bi < 0 || !golk::multi_is_il(c->multi_words, var)) continue;
-            Fam f{var, cand[bi].K, cand[bi].band, {}, {}};
+            Fam f{var, cand[bi].K, cand[bi].band, cand[bi].tw, cand[bi].seg, {}, {}};
+            if (var == golk::kMultiTile) {       // (one tile shape per engine: this one)
+                c->tile_w = f.tw;
+                c->tile_seg = f.seg;
+            }
             for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k) {
                 f.T[k] = 0.f;
                 f.band_k[k] = 0;
@@ -769,7 +811,8 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                     continue;
                 f.band_k[k] = band_same_rounds(c, var, f.K, f.band, k);
                 for (int pass = 0; pass < 2; ++pass) {
-                    const float v = time_one(Cand{var, k, f.band_k[k]}, reps) * (float)k;
+                    const float v =
+                        time_one(Cand{var, k, f.band_k[k], f.tw, f.seg}, reps) * (float)k;
                     if (v > 0.f && (f.T[k] == 0.f || v < f.T[k])) f.T[k] = v;
                 }
             }
@@ -810,6 +853,10 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     c->multi_variant = pick.var;
     c->tpl = pick.K;
     c->band_multi = pick.band;
+    if (pick.var == golk::kMultiTile) {
+        c->tile_w = pick.tw;
+        c->tile_seg = pick.seg;
+    }
     for (int &b : c->band_at) b = 0;
     c->plan = std::move(plan);
     c->tuned_us_per_turn = best * 1000.f;
@@ -959,11 +1006,13 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         c->registered = true;
     }
     c->stream = c->own_stream;
-    // small boards: k_step_tile (kMultiTile) at the model's best shape for the requested or
-    // default depth; the autotune below times the model's best shapes
+    // small boards (and k_step_tile pinned by GOL_MULTI_VARIANT): k_step_tile at the model's
+    // best shape for the requested or default depth; the autotune below times the model's best
+    // shapes
     const bool small = c->fast && c->tpl > 1 && (long long)c->buf_rows * c->pitch < (1ll << 20);
     const bool pinned = getenv("GOL_MULTI_VARIANT") != nullptr;
-    if (small && ((!pinned && cfg->band_rows <= 0) || c->multi_variant == golk::kMultiTile)) {
+    if (c->fast && c->tpl > 1 &&
+        ((small && !pinned && cfg->band_rows <= 0) || c->multi_variant == golk::kMultiTile)) {
         int K = cfg->turns_per_launch > 0 ? std::min(cfg->turns_per_launch, 32) : 0;
         if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) K = std::max(2, std::min(atoi(v), 32));
         std::vector<TileShape> cand = tile_candidates(c->ncu, c->nw, c->buf_rows, 1 << 20);
@@ -994,8 +1043,6 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         if (c->multi_variant == golk::kMultiTile &&
             !golk::tile_shape_ok(c->nw, c->tpl, c->band_multi, c->tile_w, c->tile_seg))
             return bail(GOL_EINVAL);
-    } else if (c->multi_variant == golk::kMultiTile) {
-        return bail(GOL_EINVAL);             // k_step_tile: boards below 2^20 words only
     }
     if (small && c->multi_variant == golk::kMultiTile && !pinned && cfg->band_rows <= 0 &&
         cfg->turns_per_launch <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {

@@ -181,6 +181,7 @@ int pick_band_multi(int width, int rows, int lane_dwords, int turns, int capacit
 hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 // k_step_tile (gol_tile.hip): a launch of `turns` turns on tiles of band x tile_w words with
 // tile_seg rows per lane; shape check, workgroup waves, tile count
+constexpr int kTileMaxWavesHost = 16;  // k_step_tile: waves per workgroup (gol_tile.h)
 bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg);
 int tile_waves(int turns, int tile_h, int tile_w, int seg);
 long long tile_count(int nw, int rows, int tile_h, int tile_w);

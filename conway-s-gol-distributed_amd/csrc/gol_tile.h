@@ -17,30 +17,37 @@
 //     between turns.  Horizontal neighbours come from the adjacent lanes by DPP (the lanes
 //     at a group edge read another group's word: only the halo columns see that); the
 //     1-bit funnel shifts and the 7-op rule are K1s's (gol_device.h, life_rule7).
-//   * Vertical neighbours.  Per turn each lane publishes its segment's first and last row
-//     in LDS (double-buffered by turn parity: one barrier per turn), then reads the row
-//     above its segment (the previous segment's last) and the row below (the next one's
+//   * Vertical neighbours.  Per turn each lane sums its segment's first and last row (the
+//     3-cell horizontal sums every rule needs) and publishes the two sums in LDS
+//     (double-buffered by turn parity: one barrier per turn), then reads the sums of the row
+//     above its segment (the previous segment's last) and of the row below (the next one's
 //     first), and sweeps its segment top to bottom with a 3-row window of row sums,
-//     overwriting each row in place once its sums are taken.
+//     overwriting each row in place once its sums are taken.  Every row is summed once per
+//     turn (exchanging raw rows cost each lane 2 extra row sums a turn: +33 % at SEG = 4).
 //   * After K turns the lanes holding interior rows and columns store them.
-// Work per turn and lane: (SEG + 2) row sums (2 DPP, 2 v_alignbit, 4 v_bitop3) + SEG rules
-// (14 v_bitop3) + 4 LDS accesses; waste = the (TH + 2K) / TH halo rows, C / TW halo columns
-// and the 64 - G C idle lanes.  The host (tile_plan) picks TW, TH, SEG and K.
+// Work per turn and lane: SEG row sums (2 DPP, 2 v_alignbit, 4 v_bitop3) + SEG rules
+// (14 v_bitop3) + 4 16-B LDS accesses; waste = the (TH + 2K) / TH halo rows, C / TW halo
+// columns and the 64 - G C idle lanes.  The engine (tile_candidates + autotune) picks TW, TH,
+// SEG and K.
 #pragma once
 #include "gol_device.h"
 
 namespace golk {
 
 constexpr int kTileMaxWaves = 16;                       // 1024 threads per workgroup
-constexpr int kTileXch = kTileMaxWaves * 64;            // LDS exchange slots (segments x C)
+// dynamic LDS of a workgroup of `threads` threads: row sums of the segments' edge rows,
+// first and last row, two turn parities, 16 B each
+constexpr size_t tile_lds_bytes(int threads) { return (size_t)threads * 4 * 16; }
 
 template <int SEG>
 __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restrict__ in,
                                                      uint64_t *__restrict__ out, StepArgs a,
                                                      int turns, int ntx, int ntiles)
 {
-    // per turn parity: the first / last row of every segment (segment-major, C per segment)
-    __shared__ uint2 xtop[2][kTileXch], xbot[2][kTileXch];
+    // per turn parity: the 3-cell row sums (4 dwords) of the first / last row of every segment,
+    // segment-major, C slots per segment (dynamic LDS: 2 x 2 x waves x 64 x 16 B)
+    extern __shared__ uint4 xsh[];
+    const int nslot = (int)(blockDim.x);                 // waves x 64 >= segments x C
     const int TW = a.tile_w, C = TW + 2, G = 64 / C;
     const int K = turns, TH = a.band;
     // XCD-aware tile order: blockIdx b runs on XCD b % 8, which gets a contiguous run of
@@ -97,33 +104,50 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
         s[2] = xor3(x[0], x[1], er1);
         s[3] = maj(x[0], x[1], er1);
     };
+    uint4 *xtop[2] = {xsh, xsh + nslot};
+    uint4 *xbot[2] = {xsh + 2 * nslot, xsh + 3 * nslot};
     const bool has_up = seg > 0, has_dn = seg + 1 < nseg;
     for (int t = 0; t < K; ++t) {
         const int p = t & 1;
+        // the segment's first and last row sums go to the neighbours (row sums, not rows: no
+        // lane sums a row twice -- SEG row sums and SEG rules per turn)
+        uint32_t F[4], Lr[4];
+        rsum(v[0], F);
+        if (SEG > 1) rsum(v[SEG - 1], Lr);
+        else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Lr[k] = F[k];
+        }
         if (live) {
-            xtop[p][slot] = make_uint2(v[0][0], v[0][1]);
-            xbot[p][slot] = make_uint2(v[SEG - 1][0], v[SEG - 1][1]);
+            xtop[p][slot] = make_uint4(F[0], F[1], F[2], F[3]);
+            xbot[p][slot] = make_uint4(Lr[0], Lr[1], Lr[2], Lr[3]);
         }
         __syncthreads();
-        uint32_t up[2] = {0, 0}, dn[2] = {0, 0};
+        uint32_t A[4] = {0, 0, 0, 0}, D[4] = {0, 0, 0, 0};
         if (live && has_up) {
-            const uint2 u = xbot[p][slot - C];
-            up[0] = u.x;
-            up[1] = u.y;
+            const uint4 u = xbot[p][slot - C];
+            A[0] = u.x; A[1] = u.y; A[2] = u.z; A[3] = u.w;
         }
         if (live && has_dn) {
-            const uint2 d = xtop[p][slot + C];
-            dn[0] = d.x;
-            dn[1] = d.y;
+            const uint4 d = xtop[p][slot + C];
+            D[0] = d.x; D[1] = d.y; D[2] = d.z; D[3] = d.w;
         }
-        uint32_t A[4], B[4];
-        rsum(up, A);
-        rsum(v[0], B);
+        // sweep: A = sums of the row above, B = this row's, Cs = the row below's
+        uint32_t B[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) B[k] = F[k];
 #pragma unroll
         for (int i = 0; i < SEG; ++i) {
             uint32_t Cs[4];
-            if (i + 1 < SEG) rsum(v[i + 1], Cs);
-            else rsum(dn, Cs);
+            if (i + 1 == SEG) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) Cs[k] = D[k];
+            } else if (i + 2 == SEG) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) Cs[k] = Lr[k];
+            } else {
+                rsum(v[i + 1], Cs);
+            }
             const uint32_t n0 = life_rule7(A[0], B[0], Cs[0], A[1], B[1], Cs[1], v[i][0]);
             const uint32_t n1 = life_rule7(A[2], B[2], Cs[2], A[3], B[3], Cs[3], v[i][1]);
             v[i][0] = n0;

@@ -59,7 +59,7 @@ hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s)
     uint64_t *out = a.out;
     int k = turns, ntx_arg = ntx, nt = (int)ntiles;
     void *params[] = {&in, &out, &args, &k, &ntx_arg, &nt};
-    return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params, 0, s);
+    return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params, tile_lds_bytes(threads), s);
 }
 
 }  // namespace golk

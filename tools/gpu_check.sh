@@ -43,8 +43,14 @@ for step in "$@"; do
     c2def)  run c2def 300 python -u bench.py --size 5120 --steps 1000 --warmup 40 --c3-size 0 --no-cpu-baseline ;;
     c2sweep) run c2sweep 500 python -u tools/sweep.py --size 5120 --variants 2 --bands 16,24,32,48,64 --tpl 4,8,12,16 --mw 1 --mv 7,9,12 --turns 960 ;;
     sq65)   run sq65 300 bash tools/pmc_sq.sh ;;
+    full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
+    bench20) run bench20 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     newt)   run newt 400 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "tile or small_board or rejects_tools or spin_timeout or snapshot_while or control_word or 5120 or random_vs_oracle" ;;
-    c2tile) run c2tile 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --shapes 10:160:4:32,10:160:4:16,10:160:3:24,10:160:8:32,10:80:4:16,10:80:2:12,16:160:4:24,14:160:4:24,20:320:4:32,40:320:8:32 ;;
+    c2tile) run c2tile 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --shapes 10:160:4:32,10:160:4:16,10:160:3:24,10:160:8:32,10:80:4:16,10:80:2:12,16:160:4:24,14:160:4:24,20:320:4:32,10:160:12:32,10:320:16:32,30:320:16:16,10:96:2:32,10:128:2:16,10:64:2:16,10:160:2:24,14:128:2:16,6:128:3:16,6:96:2:16 ;;
+    autolog) run autolog 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 && run autolog16 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 16384 --auto --turns 960 && run autolog65 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 65536 --auto --turns 64 --rounds 2 ;;
+    sqtile) run sqtile 300 bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 32 --band 576 --tile 30,40 --turns 128 && run sqskew 300 env TAG=_skew bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 7 --tpl 10 --band 137 --turns 100 ;;
+    bigtile) run bigtile 300 python -u tools/tile_sweep.py --size 16384 --turns 320 --shapes 30:586:40:32,30:586:48:32,62:512:40:32,62:400:32:32,14:900:16:24,30:300:24:16 ;;
+    bigtile65) run bigtile65 300 python -u tools/tile_sweep.py --size 65536 --turns 64 --rounds 2 --shapes 62:576:40:32,30:576:40:32,62:448:32:32,14:900:16:24,62:700:48:16 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done
