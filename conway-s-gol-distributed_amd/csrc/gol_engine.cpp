@@ -26,6 +26,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -172,6 +173,25 @@ struct DeviceGuard {
 // on one device).  The rows it would have published are recomputed as plain helix bands.
 std::mutex g_dev_mu;
 std::map<int, int> g_dev_engines;
+
+// Create-time autotune results, per (device, width, buffer rows, requested depth, what was
+// tuned): engines of one shape in one process -- the strips of a run, the engines a test suite
+// or a sweep creates -- time their candidates once (GOL_AUTOTUNE_CACHE=0: always re-time).
+struct TuneKey {
+    int dev, width, rows, tpl_req, mode;
+    bool operator<(const TuneKey &o) const
+    {
+        return std::tie(dev, width, rows, tpl_req, mode) <
+               std::tie(o.dev, o.width, o.rows, o.tpl_req, o.mode);
+    }
+};
+struct TuneVal {
+    int var, tpl, band, tile_w, tile_seg;
+    float us;
+    std::vector<Launch> plan;
+};
+std::mutex g_tune_mu;
+std::map<TuneKey, TuneVal> g_tune;
 
 bool device_exclusive(int dev)
 {
@@ -457,20 +477,19 @@ struct TileShape {
 // 4 half-rate v_alignbit / DPP moves per row pair); a SIMD shares its issue between its
 // resident waves, one wave alone issues at most every ~5 cycles, and each turn adds a barrier
 // and the LDS exchange -- cheaper to hide with >= 2 workgroups per CU (~80 % of the issue
-// rate and ~700 cycles a turn) than with one (~70 %, ~900).  A workgroup of `seg` rows per
-// lane holds ~2 seg + 30 VGPRs.
+// rate and ~700 cycles a turn) than with one (~70 %, ~900).  Residency from the occupancy
+// API (the kernel's VGPRs and dynamic LDS).
 double tile_model_us(int ncu, int nw, int rows, int K, int th, int tw, int seg)
 {
     if (!golk::tile_shape_ok(nw, K, th, tw, seg)) return 0;
-    const long long tiles = golk::tile_count(nw, rows, th, tw);
+    const long long tiles = golk::tile_count(nw, rows, th, tw, seg);
     const int waves = golk::tile_waves(K, th, tw, seg);
-    const int vgpr = (2 * seg + 30 + 7) / 8 * 8;
-    const int wps_max = std::min(8, 512 / vgpr);                      // waves per SIMD
-    const int wgpc = std::max(1, std::min(4 * wps_max / waves, 5));    // (32 KB LDS each)
+    const int wgpc = golk::tile_blocks_per_cu(K, th, tw, seg);         // VGPRs, LDS
+    if (wgpc <= 0) return 0;
     const long long slots = (long long)ncu * wgpc;
     const long long rounds = (tiles + slots - 1) / slots;
     const long long per_cu = std::min<long long>((tiles + ncu - 1) / ncu, wgpc);
-    const double instr = (seg + 2) * 8.0 + seg * 14.0;                 // per wave and turn
+    const double instr = (seg % 100) * 22.0;                           // per wave and turn
     const double issue = (double)(per_cu * waves) * instr * 2.36 / 4.0;
     const bool two = per_cu >= 2;
     const double turn_cyc = std::max(issue / (two ? 0.8 : 0.7), instr * 5.0) + (two ? 700 : 900);
@@ -484,7 +503,9 @@ double tile_model_us(int ncu, int nw, int rows, int K, int th, int tw, int seg)
 // resident tiles per CU or a few more tile rows.
 std::vector<TileShape> tile_candidates(int ncu, int nw, int rows, int keep)
 {
-    static const int kSegs[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48};
+    // SEG, and SEG + 100 for the interior-rows-first turn order (gol_tile.hip)
+    static const int kSegs[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
+                                106, 108, 112, 116, 124, 132, 140};
     std::vector<TileShape> all;
     std::vector<int> tws;
     for (int ntx = 1; ntx <= nw; ++ntx) {
@@ -497,7 +518,7 @@ std::vector<TileShape> tile_candidates(int ncu, int nw, int rows, int keep)
             const int C = tw + 2, G = 64 / C;
             const long long ntx = (nw + tw - 1) / tw;
             for (int seg : kSegs) {
-                const int thmax = golk::kTileMaxWavesHost * G * seg - 2 * K;
+                const int thmax = golk::kTileMaxWavesHost * G * (seg % 100) - 2 * K;
                 if (thmax < 1) continue;
                 std::vector<long long> ntys;
                 const long long nty0 = (rows + thmax - 1) / thmax;
@@ -540,34 +561,72 @@ void apply_tile(gol_ctx *c, const TileShape &t)
     c->plan.clear();
 }
 
-// Boards below 2^20 words (5120^2: 409 600) cannot fill the GPU with band pipelines: time the
-// model's best k_step_tile shapes on the engine's own buffers and keep the fastest.
-void autotune_small(gol_ctx *c)
+// Measured search for the k_step_tile shape (coordinate descent over the launch parameters;
+// the model above only seeds the widths): from (the best-filled tile width, 8 waves per
+// workgroup, K = 32 or the requested depth, SEG 16), improve one parameter at a time -- SEG
+// (both turn orders), tile width, waves per workgroup (the tile height follows: the tallest
+// tile that many waves hold), K -- and keep each improvement.  The grid sweeps of
+// profiles/r03_tile_grid_*.log put the best shapes at 8-wave workgroups (2 per CU) at every
+// board size, with SEG from 4-6 (5120^2) to 16-40 (65536^2).  Returns the best measured
+// shape (K == 0: none ran) and its time per turn in *us.
+TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
 {
-    std::vector<TileShape> cand = tile_candidates(c->ncu, c->nw, c->buf_rows, 20);
-    if (cand.empty()) return;
+    *us = 0.f;
+    const int nw = c->nw, rows = c->buf_rows;
+    if (nw % W) return TileShape{};
+    const int nl = nw / W;                           // lane columns (W words each)
+    struct WOpt { double useful; int tw; };
+    std::vector<WOpt> wopt;
+    for (int tw = 1; tw <= 62; ++tw) {
+        const int G = 64 / (tw + 2);
+        const long long ntx = (nl + tw - 1) / tw;
+        wopt.push_back({(double)G * tw / 64.0 * nl / (double)(ntx * tw), tw});
+    }
+    std::sort(wopt.begin(), wopt.end(), [](const WOpt &x, const WOpt &y) {
+        return x.useful > y.useful || (x.useful == y.useful && x.tw > y.tw);
+    });
+    std::vector<int> tws;
+    for (const WOpt &w : wopt)
+        if ((int)tws.size() < 3 && w.useful >= wopt[0].useful * 0.9) tws.push_back(w.tw);
+    static const int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
+                                 106, 108, 112, 116, 124, 132, 140};
+    static const int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1012, 1016,
+                                 1106, 1108, 1112, 1116};
+    std::vector<int> segs = W == 1 ? std::vector<int>(std::begin(kSegs1), std::end(kSegs1))
+                                   : std::vector<int>(std::begin(kSegs2), std::end(kSegs2));
+    struct P { int K, wv, tw, seg; };
+    auto shape = [&](const P &p) -> TileShape {
+        const int G = 64 / (p.tw + 2);
+        int th = p.wv * G * (p.seg % 100) - 2 * p.K;
+        th = std::min(th, rows);
+        if (th < std::min(8, rows) ||
+            !golk::tile_shape_ok(nw, p.K, th, p.tw, p.seg))
+            return TileShape{};
+        return TileShape{p.K, th, p.tw, p.seg, 0};
+    };
     golk::StepArgs a{};
     a.width = c->cfg.width;
-    a.nw = c->nw;
+    a.nw = nw;
     a.pitch = c->pitch;
-    a.modrows = c->buf_rows;
+    a.modrows = rows;
     a.row_lo = 0;
-    a.row_hi = c->buf_rows;
+    a.row_hi = rows;
     a.multi_words = 1;
     a.multi_variant = golk::kMultiTile;
     a.err = c->d_err;
-    if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
-                                 c->buf_rows, 12345, c->stream) != hipSuccess)
-        return;
+    if (golk::launch_fill_random(c->board[0], c->cfg.width, nw, c->pitch, rows, 0, rows, 12345,
+                                 c->stream) != hipSuccess)
+        return TileShape{};
     hipEvent_t e0, e1;
-    if (hipEventCreate(&e0) != hipSuccess) return;
-    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
-    auto time_one = [&](const TileShape &t, int reps) -> float {
+    if (hipEventCreate(&e0) != hipSuccess) return TileShape{};
+    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return TileShape{}; }
+    int reps = 16;
+    auto time_one = [&](const TileShape &t, int n) -> float {
         a.band = t.th;
         a.tile_w = t.tw;
         a.tile_seg = t.seg;
         bool ok = hipEventRecord(e0, c->stream) == hipSuccess;
-        for (int rep = 0; rep < reps && ok; ++rep) {
+        for (int rep = 0; rep < n && ok; ++rep) {
             a.in = c->board[rep & 1];
             a.out = c->board[(rep + 1) & 1];
             ok = golk::launch_step_multi(a, t.K, c->stream) == hipSuccess;
@@ -576,29 +635,88 @@ void autotune_small(gol_ctx *c)
              hipEventSynchronize(e1) == hipSuccess;
         float ms = 0.f;
         if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return 0.f;
-        return ms / ((float)reps * t.K);
+        return ms / ((float)n * t.K);
     };
-    (void)time_one(cand[0], 40);             // clock ramp
-    std::vector<float> t(cand.size(), 0.f);
-    for (int pass = 0; pass < 2; ++pass)
-        for (size_t i = 0; i < cand.size(); ++i) {
-            const float v = time_one(cand[i], 16);
-            if (v > 0.f && (t[i] == 0.f || v < t[i])) t[i] = v;
+    std::map<std::tuple<int, int, int, int>, float> memo;
+    auto measure = [&](const P &p) -> float {
+        const TileShape t = shape(p);
+        if (!t.K) return 0.f;
+        auto key = std::make_tuple(t.K, t.th, t.tw, t.seg);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+        float best = 0.f;
+        for (int pass = 0; pass < 2; ++pass) {      // best of two (clock noise)
+            const float v = time_one(t, reps);
+            if (v > 0.f && (best == 0.f || v < best)) best = v;
         }
+        memo[key] = best;
+        if (getenv("GOL_AUTOTUNE_LOG"))
+            fprintf(stderr, "autotune tile %dx%d K=%d th=%d tw=%d seg=%d us_per_turn=%.4f\n",
+                    c->cfg.width, rows, t.K, t.th, t.tw, t.seg, best * 1000.f);
+        return best;
+    };
+    P cur{kfix > 0 ? kfix : 32, 8, tws.empty() ? 30 : tws[0], W == 1 ? 16 : 1008};
+    // clock ramp, and the repetitions that make a measurement ~0.5 ms of launches
+    {
+        TileShape t0 = shape(cur);
+        if (!t0.K) {                          // (tiny boards: shallower SEG)
+            for (int sg : {8, 4, 2}) {
+                cur.seg = sg + 1000 * (W - 1);
+                if ((t0 = shape(cur)).K) break;
+            }
+        }
+        if (t0.K) {
+            const float v = time_one(t0, 8) * 1000.f * t0.K;   // us per launch
+            if (v > 0.f) reps = std::max(2, std::min(16, (int)(500.f / v) + 1));
+            (void)time_one(t0, reps);
+        }
+    }
+    float best = measure(cur);
+    auto improve = [&](P p) {
+        const float v = measure(p);
+        if (v > 0.f && (best == 0.f || v < best * 0.995f)) {
+            best = v;
+            cur = p;
+        }
+    };
+    {
+        const P base = cur;
+        for (int sg : segs) improve(P{base.K, base.wv, base.tw, sg});
+    }
+    {
+        const P base = cur;
+        for (int tw : tws) improve(P{base.K, base.wv, tw, base.seg});
+    }
+    {
+        const P base = cur;
+        for (int wv : {4, 6, 8, 12, 16}) improve(P{base.K, wv, base.tw, base.seg});
+    }
+    if (kfix <= 0) {
+        const P base = cur;
+        for (int K : {12, 16, 20, 24, 32}) improve(P{K, base.wv, base.tw, base.seg});
+    }
+    {
+        const P base = cur;
+        for (int sg : segs) improve(P{base.K, base.wv, base.tw, sg});
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipGetLastError();
-    int bi = -1;
-    for (size_t i = 0; i < cand.size(); ++i) {
-        if (getenv("GOL_AUTOTUNE_LOG"))
-            fprintf(stderr, "autotune tile %dx%d K=%d th=%d tw=%d seg=%d model=%.3f us=%.3f\n",
-                    c->cfg.width, c->buf_rows, cand[i].K, cand[i].th, cand[i].tw, cand[i].seg,
-                    cand[i].model_us, t[i] * 1000.f);
-        if (t[i] > 0.f && (bi < 0 || t[i] < t[(size_t)bi])) bi = (int)i;
-    }
-    if (bi < 0) return;
-    apply_tile(c, cand[(size_t)bi]);
-    c->tuned_us_per_turn = t[(size_t)bi] * 1000.f;
+    *us = best * 1000.f;
+    return best > 0.f ? shape(cur) : TileShape{};
+}
+
+// Boards below 2^20 words (5120^2: 409 600) cannot fill the GPU with band pipelines: they run
+// k_step_tile at the measured-best shape.
+void autotune_small(gol_ctx *c)
+{
+    float us1 = 0.f, us2 = 0.f;
+    const TileShape t1 = tile_search(c, 0, &us1, 1);
+    const TileShape t2 = tile_search(c, 0, &us2, 2);   // two words per lane
+    const bool two = t2.K && (!t1.K || us2 < us1);
+    if (!t1.K && !t2.K) return;
+    apply_tile(c, two ? t2 : t1);
+    c->tuned_us_per_turn = two ? us2 : us1;
 }
 
 // Create-time timing sweep of the temporal-blocking kernel, its depth K and its band on
@@ -625,12 +743,11 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     std::vector<Cand> cand;
     for (int var : vars) {
         if (var == golk::kMultiTile) {
-            // the model's best tile shapes (their own K and height), timed like the rest
-            int kept = 0;
-            for (const TileShape &ts : tile_candidates(ncu, c->nw, c->buf_rows, 64)) {
-                if (!tune_k && ts.K != c->tpl) continue;
-                cand.push_back({var, ts.K, ts.th, ts.tw, ts.seg});
-                if (++kept == 10) break;
+            // the measured-best tile shape (tile_search), timed again beside the rest
+            for (int W : {1, 2}) {
+                float us = 0.f;
+                const TileShape ts = tile_search(c, tune_k ? 0 : c->tpl, &us, W);
+                if (ts.K) cand.push_back({var, ts.K, ts.th, ts.tw, ts.seg});
             }
             continue;
         }
@@ -805,8 +922,9 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k) {
                 f.T[k] = 0.f;
                 f.band_k[k] = 0;
-                // (k_step_wg runs depths 2, 3 as k_step_skew: that family covers them)
-                if (k > 16 || !golk::multi_ok(c->cfg.width, k, var) ||
+                // (k_step_wg runs depths 2, 3 as k_step_skew: that family covers them; the
+                // tile kernel's depth is a runtime loop: it is timed up to 32)
+                if ((k > 16 && var != golk::kMultiTile) || !golk::multi_ok(c->cfg.width, k, var) ||
                     (golk::is_wg_variant(var) && k < 4))
                     continue;
                 f.band_k[k] = band_same_rounds(c, var, f.K, f.band, k);
@@ -834,7 +952,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                 }
         if (getenv("GOL_AUTOTUNE_LOG")) {
             for (const Fam &f : fams)
-                for (int k = 2; k <= 16; ++k)
+                for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k)
                     if (f.T[k] > 0.f)
                         fprintf(stderr, "autotune launch var=%d K=%d band=%d us=%.1f\n", f.var, k,
                                 f.band_k[k], f.T[k] * 1000.f);
@@ -1044,21 +1162,48 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
             !golk::tile_shape_ok(c->nw, c->tpl, c->band_multi, c->tile_w, c->tile_seg))
             return bail(GOL_EINVAL);
     }
-    if (small && c->multi_variant == golk::kMultiTile && !pinned && cfg->band_rows <= 0 &&
-        cfg->turns_per_launch <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {
-        const char *at = getenv("GOL_AUTOTUNE");
-        if (!at || atoi(at) != 0) autotune_small(c);
-        if (int rc2 = check_dev_err(c)) return bail(rc2);
-    } else if (c->tpl > 1 && cfg->band_rows <= 0 && !(cfg->flags & GOL_FLAG_NO_AUTOTUNE)) {
-        const char *at = getenv("GOL_AUTOTUNE");
-        // the kernel is tuned too unless an experiment pins it (GOL_MULTI_VARIANT) or the
-        // requested depth only one of them runs
-        const bool tune_var = !getenv("GOL_MULTI_VARIANT") && c->multi_words == 1 &&
-                              (cfg->turns_per_launch <= 0 || cfg->turns_per_launch <= 8);
-        if (!at || atoi(at) != 0) autotune_multi(c, cfg->turns_per_launch <= 0, tune_var);
+    const char *at = getenv("GOL_AUTOTUNE");
+    const bool tuning = !(cfg->flags & GOL_FLAG_NO_AUTOTUNE) && (!at || atoi(at) != 0) &&
+                        cfg->band_rows <= 0 && c->tpl > 1;
+    const bool tune_small = small && c->multi_variant == golk::kMultiTile && !pinned &&
+                            cfg->turns_per_launch <= 0;
+    // the kernel is tuned too unless an experiment pins it (GOL_MULTI_VARIANT) or the requested
+    // depth only one of them runs
+    const bool tune_var = !pinned && c->multi_words == 1 &&
+                          (cfg->turns_per_launch <= 0 || cfg->turns_per_launch <= 8);
+    const TuneKey key{dev, cfg->width, c->buf_rows, cfg->turns_per_launch,
+                      (tune_small ? 4 : 0) | (tune_var ? 2 : 0) | (pinned ? 1 : 0) |
+                          (c->multi_variant << 3)};
+    const char *tc = getenv("GOL_AUTOTUNE_CACHE");
+    const bool use_cache = !tc || atoi(tc) != 0;
+    bool cached = false;
+    if (tuning && use_cache) {
+        std::lock_guard<std::mutex> lk(g_tune_mu);
+        auto it = g_tune.find(key);
+        if (it != g_tune.end()) {
+            const TuneVal &v = it->second;
+            c->multi_variant = v.var;
+            c->tpl = v.tpl;
+            c->band_multi = v.band;
+            c->tile_w = v.tile_w;
+            c->tile_seg = v.tile_seg;
+            c->plan = v.plan;
+            c->tuned_us_per_turn = v.us;
+            for (int &b : c->band_at) b = 0;
+            cached = true;
+        }
+    }
+    if (tuning && !cached && (tune_small || !small)) {
+        if (tune_small) autotune_small(c);
+        else autotune_multi(c, cfg->turns_per_launch <= 0, tune_var);
         // a wait that gave up while timing the candidates: fail loudly at create
         (void)hipStreamSynchronize(c->stream);
         if (check_dev_err(c)) return bail(GOL_EHIP);
+        if (use_cache) {
+            std::lock_guard<std::mutex> lk(g_tune_mu);
+            g_tune[key] = TuneVal{c->multi_variant, c->tpl, c->band_multi, c->tile_w,
+                                  c->tile_seg, c->tuned_us_per_turn, c->plan};
+        }
     }
     if ((e = hipMemsetAsync(c->board[0], 0, words * 8, c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->board[1], 0, words * 8, c->stream)) != hipSuccess ||

@@ -184,7 +184,9 @@ hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 constexpr int kTileMaxWavesHost = 16;  // k_step_tile: waves per workgroup (gol_tile.h)
 bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg);
 int tile_waves(int turns, int tile_h, int tile_w, int seg);
-long long tile_count(int nw, int rows, int tile_h, int tile_w);
+// resident workgroups per CU of that launch (occupancy API: VGPRs, LDS; 0 on error)
+int tile_blocks_per_cu(int turns, int tile_h, int tile_w, int seg);
+long long tile_count(int nw, int rows, int tile_h, int tile_w, int seg);
 hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);

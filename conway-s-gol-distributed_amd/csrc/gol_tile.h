@@ -35,21 +35,32 @@
 namespace golk {
 
 constexpr int kTileMaxWaves = 16;                       // 1024 threads per workgroup
-// dynamic LDS of a workgroup of `threads` threads: row sums of the segments' edge rows,
-// first and last row, two turn parities, 16 B each
-constexpr size_t tile_lds_bytes(int threads) { return (size_t)threads * 4 * 16; }
+// dynamic LDS of a workgroup of `threads` threads: row sums of the segments' edge rows (16 B
+// per word of the lane), first and last row, two turn parities
+constexpr size_t tile_lds_bytes(int threads, int words) { return (size_t)threads * 4 * 16 * words; }
+// tile_seg = SEG + 100 * ORD + 1000 * (W - 1): rows per lane segment, turn order, words per lane
+constexpr int tile_seg_rows(int code) { return code % 100; }
+constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 
-template <int SEG>
+// W words per lane (2W dwords, interleaved layout word by word).  With W = 2 the lane's two
+// words are neighbours, so only the outer edges need a lane shift: per row 2 DPP + 2W funnel
+// shifts + 4W v_bitop3 instead of W x (2 + 2 + 4) -- 48 instead of 52 SIMD cycles per 4096
+// cell-updates with the rule.
+template <int SEG, int ORD, int W>
 __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restrict__ in,
                                                      uint64_t *__restrict__ out, StepArgs a,
                                                      int turns, int ntx, int ntiles)
 {
-    // per turn parity: the 3-cell row sums (4 dwords) of the first / last row of every segment,
-    // segment-major, C slots per segment (dynamic LDS: 2 x 2 x waves x 64 x 16 B)
+    constexpr int ND = 2 * W;                            // dwords per lane and row
+    constexpr int NS = 2 * ND;                           // row-sum dwords (2 bits per dword)
+    static_assert(SEG >= 2, "two edge rows per segment");
+    // per turn parity: the 3-cell row sums of the first / last row of every segment,
+    // segment-major, C slots per segment (dynamic LDS, W uint4 per slot)
     extern __shared__ uint4 xsh[];
     const int nslot = (int)(blockDim.x);                 // waves x 64 >= segments x C
-    const int TW = a.tile_w, C = TW + 2, G = 64 / C;
+    const int TW = a.tile_w, C = TW + 2, G = 64 / C;     // (in lanes of W words)
     const int K = turns, TH = a.band;
+    const int nl = a.nw / W;                             // lane columns per row
     // XCD-aware tile order: blockIdx b runs on XCD b % 8, which gets a contiguous run of
     // tiles (whole tile rows, so most halo rows were written by the same XCD's L2)
     const int per = (ntiles + 7) / 8;
@@ -66,113 +77,180 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
     const int nseg = (TH + 2 * K + SEG - 1) / SEG;       // segments the tile needs
     const int slot = seg * C + col;
 
-    // word column (torus wrap) and the lane's rows: tile row t = seg * SEG + i is buffer row
+    // lane column (torus wrap) and the lane's rows: tile row t = seg * SEG + i is buffer row
     // y0 - K + t (mod modrows; rows past the tile are read, never stored)
     int gx = x0 - 1 + (live ? col : 0);
-    while (gx < 0) gx += a.nw;
-    while (gx >= a.nw) gx -= a.nw;
+    while (gx < 0) gx += nl;
+    while (gx >= nl) gx -= nl;
     const int M = a.modrows;
     const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
     const uint32_t span = (uint32_t)M * pitch_b;
     int r = y0 - K + (live ? seg : 0) * SEG;
     while (r < 0) r += M;
     while (r >= M) r -= M;
-    uint32_t off = (uint32_t)r * pitch_b + (uint32_t)gx * 8u;
+    uint32_t off = (uint32_t)r * pitch_b + (uint32_t)gx * (8u * W);
     const __amdgpu_buffer_rsrc_t rin =
         __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)span, kBufFlags);
     const __amdgpu_buffer_rsrc_t rout =
         __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)span, kBufFlags);
 
-    uint32_t v[SEG][2];
+    uint32_t v[SEG][ND];
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
-        const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, 0);
-        v[i][0] = w.x;
-        v[i][1] = w.y;
+        if constexpr (W == 1) {
+            const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, 0);
+            v[i][0] = w.x;
+            v[i][1] = w.y;
+        } else {
+            const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+            v[i][0] = w.x;
+            v[i][1] = w.y;
+            v[i][2] = w.z;
+            v[i][3] = w.w;
+        }
         off += pitch_b;
         off = off >= span ? off - span : off;            // (the column stays < pitch_b)
     }
 
-    // 3-cell row sums of one row (even dword: s0e/s1e, odd dword: s0o/s1o): K1s's stage
-    auto rsum = [](const uint32_t (&x)[2], uint32_t (&s)[4]) {
-        const uint32_t L = dpp_from_lower_z(x[1]);       // west word's odd cells
-        const uint32_t Rt = dpp_from_upper_z(x[0]);      // east word's even cells
-        const uint32_t wl0 = __builtin_amdgcn_alignbit(x[1], L, 31);
-        const uint32_t er1 = __builtin_amdgcn_alignbit(Rt, x[0], 1);
-        s[0] = xor3(wl0, x[0], x[1]);
-        s[1] = maj(wl0, x[0], x[1]);
-        s[2] = xor3(x[0], x[1], er1);
-        s[3] = maj(x[0], x[1], er1);
+    // 3-cell row sums of one row: per word w (even dword e, odd dword o) the sums of the even
+    // cells (s[4w], s[4w+1]) and of the odd cells (s[4w+2], s[4w+3]); K1s's stage, with the
+    // neighbour words inside the lane taken as they are
+    auto rsum = [&](const uint32_t (&x)[ND], uint32_t (&s)[NS]) {
+        const uint32_t L = dpp_from_lower_z(x[ND - 1]);  // west lane's last odd cells
+        const uint32_t Rt = dpp_from_upper_z(x[0]);      // east lane's first even cells
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint32_t e = x[2 * w], o = x[2 * w + 1];
+            const uint32_t wl = __builtin_amdgcn_alignbit(o, w == 0 ? L : x[2 * w - 1], 31);
+            const uint32_t er = __builtin_amdgcn_alignbit(w == W - 1 ? Rt : x[2 * w + 2], e, 1);
+            s[4 * w + 0] = xor3(wl, e, o);
+            s[4 * w + 1] = maj(wl, e, o);
+            s[4 * w + 2] = xor3(e, o, er);
+            s[4 * w + 3] = maj(e, o, er);
+        }
     };
-    uint4 *xtop[2] = {xsh, xsh + nslot};
-    uint4 *xbot[2] = {xsh + 2 * nslot, xsh + 3 * nslot};
-    const bool has_up = seg > 0, has_dn = seg + 1 < nseg;
+    // next state of the lane's row from the sums of the rows above (A), at (B) and below (Cs)
+    auto rule = [&](const uint32_t (&A)[NS], const uint32_t (&B)[NS], const uint32_t (&Cs)[NS],
+                   uint32_t (&x)[ND]) {
+        uint32_t n[ND];
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+            n[d] = life_rule7(A[2 * d], B[2 * d], Cs[2 * d], A[2 * d + 1], B[2 * d + 1],
+                              Cs[2 * d + 1], x[d]);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) x[d] = n[d];
+    };
+    auto put = [&](uint4 *base, const uint32_t (&S)[NS]) {
+#pragma unroll
+        for (int q = 0; q < W; ++q)
+            base[(size_t)q * nslot * 4] =
+                make_uint4(S[4 * q], S[4 * q + 1], S[4 * q + 2], S[4 * q + 3]);
+    };
+    auto get = [&](const uint4 *base, bool has, uint32_t (&S)[NS]) {
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            const uint4 u = base[(size_t)q * nslot * 4];
+            S[4 * q] = has ? u.x : 0u;
+            S[4 * q + 1] = has ? u.y : 0u;
+            S[4 * q + 2] = has ? u.z : 0u;
+            S[4 * q + 3] = has ? u.w : 0u;
+        }
+    };
+    // slot arrays: [q][parity][top / bottom][slot], q = the word of the lane
+    auto xtop = [&](int p, int sl) { return xsh + (size_t)(p * 2 + 0) * nslot + sl; };
+    auto xbot = [&](int p, int sl) { return xsh + (size_t)(p * 2 + 1) * nslot + sl; };
+    const bool has_up = live && seg > 0, has_dn = live && seg + 1 < nseg;
+    // neighbour slots, clamped to a valid one where there is no neighbour (then masked to 0):
+    // the LDS reads stay unconditional, so no branch splits the turn's straight-line code
+    const int s_up = has_up ? slot - C : 0, s_dn = has_dn ? slot + C : 0;
     for (int t = 0; t < K; ++t) {
         const int p = t & 1;
         // the segment's first and last row sums go to the neighbours (row sums, not rows: no
         // lane sums a row twice -- SEG row sums and SEG rules per turn)
-        uint32_t F[4], Lr[4];
+        uint32_t F[NS], Lr[NS];
         rsum(v[0], F);
-        if (SEG > 1) rsum(v[SEG - 1], Lr);
-        else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) Lr[k] = F[k];
-        }
+        rsum(v[SEG - 1], Lr);
         if (live) {
-            xtop[p][slot] = make_uint4(F[0], F[1], F[2], F[3]);
-            xbot[p][slot] = make_uint4(Lr[0], Lr[1], Lr[2], Lr[3]);
+            put(xtop(p, slot), F);
+            put(xbot(p, slot), Lr);
         }
         __syncthreads();
-        uint32_t A[4] = {0, 0, 0, 0}, D[4] = {0, 0, 0, 0};
-        if (live && has_up) {
-            const uint4 u = xbot[p][slot - C];
-            A[0] = u.x; A[1] = u.y; A[2] = u.z; A[3] = u.w;
-        }
-        if (live && has_dn) {
-            const uint4 d = xtop[p][slot + C];
-            D[0] = d.x; D[1] = d.y; D[2] = d.z; D[3] = d.w;
-        }
-        // sweep: A = sums of the row above, B = this row's, Cs = the row below's
-        uint32_t B[4];
+        uint32_t U[NS], D[NS];
+        get(xbot(p, s_up), has_up, U);
+        get(xtop(p, s_dn), has_dn, D);
+        if constexpr (ORD == 0) {
+            // in order: A, B, Cs = sums of rows i-1, i, i+1
+            uint32_t A[NS], B[NS];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) B[k] = F[k];
+            for (int k = 0; k < NS; ++k) {
+                A[k] = U[k];
+                B[k] = F[k];
+            }
 #pragma unroll
-        for (int i = 0; i < SEG; ++i) {
-            uint32_t Cs[4];
-            if (i + 1 == SEG) {
+            for (int i = 0; i < SEG; ++i) {
+                uint32_t Cs[NS];
+                if (i + 1 == SEG) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) Cs[k] = D[k];
-            } else if (i + 2 == SEG) {
+                    for (int k = 0; k < NS; ++k) Cs[k] = D[k];
+                } else if (i + 2 == SEG) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) Cs[k] = Lr[k];
+                    for (int k = 0; k < NS; ++k) Cs[k] = Lr[k];
+                } else {
+                    rsum(v[i + 1], Cs);
+                }
+                rule(A, B, Cs, v[i]);
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    A[k] = B[k];
+                    B[k] = Cs[k];
+                }
+            }
+        } else {
+            // interior rows 1 .. SEG-2 first (their sums are all local), so the LDS reads land
+            // while they compute; window P, Q, R = sums of rows i-1, i, i+1
+            uint32_t P[NS], Q[NS], S1[NS];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) P[k] = F[k];
+            if constexpr (SEG >= 3) {
+                rsum(v[1], Q);
+#pragma unroll
+                for (int k = 0; k < NS; ++k) S1[k] = Q[k];
             } else {
-                rsum(v[i + 1], Cs);
-            }
-            const uint32_t n0 = life_rule7(A[0], B[0], Cs[0], A[1], B[1], Cs[1], v[i][0]);
-            const uint32_t n1 = life_rule7(A[2], B[2], Cs[2], A[3], B[3], Cs[3], v[i][1]);
-            v[i][0] = n0;
-            v[i][1] = n1;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                A[k] = B[k];
-                B[k] = Cs[k];
+                for (int k = 0; k < NS; ++k) S1[k] = Q[k] = Lr[k];
             }
+#pragma unroll
+            for (int i = 1; i + 1 < SEG; ++i) {
+                uint32_t R[NS];
+                if (i + 2 == SEG) {
+#pragma unroll
+                    for (int k = 0; k < NS; ++k) R[k] = Lr[k];
+                } else {
+                    rsum(v[i + 1], R);
+                }
+                rule(P, Q, R, v[i]);
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+                    P[k] = Q[k];
+                    Q[k] = R[k];
+                }
+            }
+            // (P = the sums of row SEG-2, or of row 0 when SEG == 2)
+            rule(U, F, S1, v[0]);
+            rule(P, Lr, D, v[SEG - 1]);
         }
     }
     // interior rows [K, K + TH) of the tile, below row_hi; interior columns inside the row
-    if (!live || col < 1 || col > TW || x0 + col - 1 >= a.nw) return;
+    if (!live || col < 1 || col > TW || x0 + col - 1 >= nl) return;
     const int t0 = seg * SEG;
     // per-lane byte offset (the segment differs between the lane groups of a wave); rows
     // y0 - K + t0 + i are stored only once inside [row_lo, row_hi): no wrap, and the
     // unsigned sum is exact there even if the first row of the segment lies above row 0
-    uint32_t so = (uint32_t)(y0 - K + t0) * pitch_b + (uint32_t)(x0 + col - 1) * 8u;
+    uint32_t so = (uint32_t)(y0 - K + t0) * pitch_b + (uint32_t)(x0 + col - 1) * (8u * W);
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
         const int tr = t0 + i;
-        if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) {
-            const uint32_t o[2] = {v[i][0], v[i][1]};
-            buf_store(o, rout, so, 0);
-        }
+        if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) buf_store(v[i], rout, so, 0);
         so += pitch_b;
     }
 }

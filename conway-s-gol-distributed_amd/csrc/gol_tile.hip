@@ -1,32 +1,47 @@
 // gol_tile.hip -- the k_step_tile instantiation table (K1t, gol_tile.h) and its launcher.
 #include "gol_tile.h"
 
+#include <map>
+#include <mutex>
+
 namespace golk {
 
-void *tile_kernel(int seg)
+// tile_seg = SEG + 100 * ORD + 1000 * (W - 1) (gol_tile.h): ORD 1 = the turn's interior rows
+// before the edge rows, W = words per lane
+template <int ORD, int W>
+static void *tile_fn(int seg)
 {
     switch (seg) {
-    case 2: return reinterpret_cast<void *>(&k_step_tile<2>);
-    case 3: return reinterpret_cast<void *>(&k_step_tile<3>);
-    case 4: return reinterpret_cast<void *>(&k_step_tile<4>);
-    case 6: return reinterpret_cast<void *>(&k_step_tile<6>);
-    case 8: return reinterpret_cast<void *>(&k_step_tile<8>);
-    case 12: return reinterpret_cast<void *>(&k_step_tile<12>);
-    case 16: return reinterpret_cast<void *>(&k_step_tile<16>);
-    case 24: return reinterpret_cast<void *>(&k_step_tile<24>);
-    case 32: return reinterpret_cast<void *>(&k_step_tile<32>);
-    case 40: return reinterpret_cast<void *>(&k_step_tile<40>);
-    case 48: return reinterpret_cast<void *>(&k_step_tile<48>);
+    case 2: return reinterpret_cast<void *>(&k_step_tile<2, ORD, W>);
+    case 3: return reinterpret_cast<void *>(&k_step_tile<3, ORD, W>);
+    case 4: return reinterpret_cast<void *>(&k_step_tile<4, ORD, W>);
+    case 6: return reinterpret_cast<void *>(&k_step_tile<6, ORD, W>);
+    case 8: return reinterpret_cast<void *>(&k_step_tile<8, ORD, W>);
+    case 12: return reinterpret_cast<void *>(&k_step_tile<12, ORD, W>);
+    case 16: return reinterpret_cast<void *>(&k_step_tile<16, ORD, W>);
+    case 24: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<24, ORD, 1>) : nullptr;
+    case 32: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<32, ORD, 1>) : nullptr;
+    case 40: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<40, ORD, 1>) : nullptr;
+    case 48: return W == 1 && ORD == 0 ? reinterpret_cast<void *>(&k_step_tile<48, 0, 1>) : nullptr;
     default: return nullptr;
     }
+}
+
+void *tile_kernel(int code)
+{
+    const int seg = code % 100, ord = (code / 100) % 10, w = tile_seg_words(code);
+    if (code < 0 || ord > 1 || w > 2) return nullptr;
+    if (w == 2) return ord ? tile_fn<1, 2>(seg) : tile_fn<0, 2>(seg);
+    return ord ? tile_fn<1, 1>(seg) : tile_fn<0, 1>(seg);
 }
 
 bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
 {
     if (turns < 2 || turns > 64 || tile_h < 1 || tile_w < 1 || tile_w + 2 > 64 || !tile_kernel(seg))
         return false;
-    (void)nw;
+    if (nw % tile_seg_words(seg)) return false;          // (whole word pairs per lane)
     const int C = tile_w + 2, G = 64 / C;
+    seg %= 100;
     const int nseg = (tile_h + 2 * turns + seg - 1) / seg;
     return (nseg + G - 1) / G <= kTileMaxWaves;
 }
@@ -34,13 +49,35 @@ bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
 int tile_waves(int turns, int tile_h, int tile_w, int seg)
 {
     const int C = tile_w + 2, G = 64 / C;
+    seg %= 100;
     const int nseg = (tile_h + 2 * turns + seg - 1) / seg;
     return (nseg + G - 1) / G;
 }
 
-long long tile_count(int nw, int rows, int tile_h, int tile_w)
+int tile_blocks_per_cu(int turns, int tile_h, int tile_w, int seg)
 {
-    const long long ntx = (nw + tile_w - 1) / tile_w;
+    void *fn = tile_kernel(seg);
+    if (!fn) return 0;
+    const int waves = tile_waves(turns, tile_h, tile_w, seg);
+    if (waves < 1 || waves > kTileMaxWaves) return 0;
+    // (the planner asks for thousands of shapes: cache per (kernel, waves))
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({seg, waves});
+    if (it != cache.end()) return it->second;
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks, fn, 64 * waves, tile_lds_bytes(64 * waves, tile_seg_words(seg))) != hipSuccess)
+        blocks = 0;
+    cache[{seg, waves}] = blocks;
+    return blocks;
+}
+
+long long tile_count(int nw, int rows, int tile_h, int tile_w, int seg)
+{
+    const long long nl = nw / tile_seg_words(seg);
+    const long long ntx = (nl + tile_w - 1) / tile_w;
     return ntx * ((rows + tile_h - 1) / tile_h);
 }
 
@@ -48,7 +85,7 @@ hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s)
 {
     const int rows = a.row_hi - a.row_lo;
     if (!tile_shape_ok(a.nw, turns, a.band, a.tile_w, a.tile_seg)) return hipErrorInvalidValue;
-    const int ntx = (a.nw + a.tile_w - 1) / a.tile_w;
+    const int ntx = (a.nw / tile_seg_words(a.tile_seg) + a.tile_w - 1) / a.tile_w;
     const long long ntiles = (long long)ntx * ((rows + a.band - 1) / a.band);
     if (ntiles <= 0 || ntiles > (1 << 24)) return hipErrorInvalidValue;
     const unsigned blocks = (unsigned)((ntiles + 7) / 8 * 8);
@@ -59,7 +96,8 @@ hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s)
     uint64_t *out = a.out;
     int k = turns, ntx_arg = ntx, nt = (int)ntiles;
     void *params[] = {&in, &out, &args, &k, &ntx_arg, &nt};
-    return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params, tile_lds_bytes(threads), s);
+    return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params,
+                           tile_lds_bytes(threads, tile_seg_words(a.tile_seg)), s);
 }
 
 }  // namespace golk

@@ -619,15 +619,24 @@ TILE_CASES = [
     (8320, 41, 62, 13, 4, 20, 44),        # 64-lane groups (G = 1), ragged everything
     (2048, 500, 30, 64, 8, 24, 50),       # G = 2
     (4096, 257, 5, 50, 3, 10, 33),        # C = 7: 9 groups, 1 idle lane
+    (5120, 5120, 14, 128, 106, 32, 70),   # interior rows first (ORD 1)
+    (2048, 500, 30, 64, 124, 24, 50),
+    # two words per lane (seg code + 1000): tile_w counts lanes of 2 words
+    (5120, 300, 5, 37, 1004, 16, 40),     # 40 lane columns, C = 7: 9 groups
+    (1024, 203, 7, 20, 1106, 8, 19),      # 8 lane columns: a partial last tile (1 lane)
+    (8320, 41, 30, 13, 1008, 20, 44),     # 65 lane columns: partial, G = 2
+    (256, 3, 2, 1, 1002, 24, 30),         # 2 lane columns on a 3-row torus
+    (384, 100, 3, 25, 1112, 12, 25),      # 3 lane columns: one tile, halo lanes wrap
+    (65536, 96, 14, 24, 1016, 16, 33),    # the headline width, ORD 0 at SEG 16
 ]
 
 
 @pytest.mark.parametrize("w,h,tw,th,seg,K,turns", TILE_CASES)
 def test_tile_kernel(gol, oracle, monkeypatch, w, h, tw, th, seg, K, turns):
     """k_step_tile (K turns on a register-resident 2-D tile: K halo rows, one halo word each
-    side, row segments exchanged through LDS once per turn) is bit-exact for partial tiles,
-    tiles taller than the torus, every lane grouping and turn counts leaving shallower
-    launches; read mid-run and stepped on."""
+    side, edge-row sums exchanged through LDS once per turn; 1 or 2 words per lane; both turn
+    orders) is bit-exact for partial tiles, tiles taller than the torus, every lane grouping
+    and turn counts leaving shallower launches; read mid-run and stepped on."""
     monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
     monkeypatch.setenv("GOL_TILE", f"{tw},{seg}")
     start = oracle.gen_random(w + 3 * h + K, w, h)

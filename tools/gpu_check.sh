@@ -49,6 +49,9 @@ for step in "$@"; do
     c2tile) run c2tile 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --shapes 10:160:4:32,10:160:4:16,10:160:3:24,10:160:8:32,10:80:4:16,10:80:2:12,16:160:4:24,14:160:4:24,20:320:4:32,10:160:12:32,10:320:16:32,30:320:16:16,10:96:2:32,10:128:2:16,10:64:2:16,10:160:2:24,14:128:2:16,6:128:3:16,6:96:2:16 ;;
     autolog) run autolog 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 && run autolog16 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 16384 --auto --turns 960 && run autolog65 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 65536 --auto --turns 64 --rounds 2 ;;
     sqtile) run sqtile 300 bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 32 --band 576 --tile 30,40 --turns 128 && run sqskew 300 env TAG=_skew bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 7 --tpl 10 --band 137 --turns 100 ;;
+    grid5)  run grid5 400 python -u tools/tile_sweep.py --size 5120 --turns 960 --rounds 2 --grid 10,14,8/2,3,4,6,8,106,108/16,24,32/8,12,16 ;;
+    grid16) run grid16 400 python -u tools/tile_sweep.py --size 16384 --turns 320 --rounds 2 --grid 30,14,18/8,12,16,24,32,108,112,116,124,132/16,32/8,16 ;;
+    grid65) run grid65 500 python -u tools/tile_sweep.py --size 65536 --turns 64 --rounds 2 --grid 30,14,62/16,24,32,40,116,124,132,140/16,32/8 ;;
     bigtile) run bigtile 300 python -u tools/tile_sweep.py --size 16384 --turns 320 --shapes 30:586:40:32,30:586:48:32,62:512:40:32,62:400:32:32,14:900:16:24,30:300:24:16 ;;
     bigtile65) run bigtile65 300 python -u tools/tile_sweep.py --size 65536 --turns 64 --rounds 2 --shapes 62:576:40:32,30:576:40:32,62:448:32:32,14:900:16:24,62:700:48:16 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;

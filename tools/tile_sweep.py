@@ -24,8 +24,23 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="")
     ap.add_argument("--auto", action="store_true")
+    ap.add_argument("--grid", default="",
+                    help="tws/segs/Ks/waves, e.g. '10,14/2,3,4,106/16,32/8,16': every combination, "
+                         "tile height = the tallest the workgroup of that many waves holds")
     a = ap.parse_args()
     W, H = a.size, a.height or a.size
+    if a.grid:
+        tws, segs, ks, wvs = ([int(x) for x in part.split(",")] for part in a.grid.split("/"))
+        extra = []
+        for tw in tws:
+            G = 64 // (tw + 2)
+            for seg in segs:
+                for K in ks:
+                    for wv in wvs:
+                        th = wv * G * (seg % 100) - 2 * K
+                        if th >= 8:
+                            extra.append(f"{tw}:{min(th, H)}:{seg}:{K}")
+        a.shapes = ",".join([x for x in a.shapes.split(",") if x] + extra)
     stream = torch.cuda.Stream()
     engines = {}
     for sh in [x for x in a.shapes.split(",") if x]:
