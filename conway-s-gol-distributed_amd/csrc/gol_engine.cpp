@@ -589,15 +589,17 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     for (const WOpt &w : wopt)
         if ((int)tws.size() < 3 && w.useful >= wopt[0].useful * 0.9) tws.push_back(w.tw);
     static const int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
-                                 106, 108, 112, 116, 124, 132, 140};
+                                 106, 108, 112, 116, 124, 132, 140,
+                                 203, 204, 206, 208, 212, 216, 224, 232, 240};
     static const int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1012, 1016,
-                                 1106, 1108, 1112, 1116};
+                                 1106, 1108, 1112, 1116, 1204, 1206, 1208, 1212, 1216};
     std::vector<int> segs = W == 1 ? std::vector<int>(std::begin(kSegs1), std::end(kSegs1))
                                    : std::vector<int>(std::begin(kSegs2), std::end(kSegs2));
-    struct P { int K, wv, tw, seg; };
+    struct P { int K, wv, tw, seg, th = 0; };          // th > 0: this height (<= wv's)
     auto shape = [&](const P &p) -> TileShape {
         const int G = 64 / (p.tw + 2);
         int th = p.wv * G * (p.seg % 100) - 2 * p.K;
+        if (p.th > 0) th = std::min(th, p.th);
         th = std::min(th, rows);
         if (th < std::min(8, rows) ||
             !golk::tile_shape_ok(nw, p.K, th, p.tw, p.seg))
@@ -698,6 +700,28 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     {
         const P base = cur;
         for (int sg : segs) improve(P{base.K, base.wv, base.tw, sg});
+    }
+    // round balance: the tallest tile is not always the best -- 525 tiles on 512 slots run 2
+    // rounds (8448-row strips at height 576); shorter tiles that fill the same rounds evenly
+    // take fewer waves each.  Try the heights whose tile count just fits 1..4 residency rounds.
+    {
+        const P base = cur;
+        const TileShape t0 = shape(base);
+        if (t0.K) {
+            const long long ntx = (nl + base.tw - 1) / base.tw;
+            for (int r = 1; r <= 4; ++r) {
+                for (long long nty = (rows + t0.th - 1) / t0.th; nty <= 4ll * rows; ++nty) {
+                    const int th = (int)((rows + nty - 1) / nty);
+                    if (th < 8) break;
+                    const int wg = golk::tile_blocks_per_cu(base.K, th, base.tw, base.seg);
+                    if (wg <= 0) continue;
+                    if (ntx * nty <= (long long)r * c->ncu * wg) {
+                        if (th != t0.th) improve(P{base.K, base.wv, base.tw, base.seg, th});
+                        break;
+                    }
+                }
+            }
+        }
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);

@@ -38,7 +38,9 @@ constexpr int kTileMaxWaves = 16;                       // 1024 threads per work
 // dynamic LDS of a workgroup of `threads` threads: row sums of the segments' edge rows (16 B
 // per word of the lane), first and last row, two turn parities
 constexpr size_t tile_lds_bytes(int threads, int words) { return (size_t)threads * 4 * 16 * words; }
-// tile_seg = SEG + 100 * ORD + 1000 * (W - 1): rows per lane segment, turn order, words per lane
+// tile_seg = SEG + 100 * ORD + 1000 * (W - 1): rows per lane segment, turn order (0: in order;
+// 1: interior rows, then the edge rows; 2: the same with the barrier after the interior rows),
+// words per lane
 constexpr int tile_seg_rows(int code) { return code % 100; }
 constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 
@@ -174,10 +176,12 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
             put(xtop(p, slot), F);
             put(xbot(p, slot), Lr);
         }
-        __syncthreads();
         uint32_t U[NS], D[NS];
-        get(xbot(p, s_up), has_up, U);
-        get(xtop(p, s_dn), has_dn, D);
+        if constexpr (ORD < 2) {
+            __syncthreads();
+            get(xbot(p, s_up), has_up, U);
+            get(xtop(p, s_dn), has_dn, D);
+        }
         if constexpr (ORD == 0) {
             // in order: A, B, Cs = sums of rows i-1, i, i+1
             uint32_t A[NS], B[NS];
@@ -206,8 +210,8 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
                 }
             }
         } else {
-            // interior rows 1 .. SEG-2 first (their sums are all local), so the LDS reads land
-            // while they compute; window P, Q, R = sums of rows i-1, i, i+1
+            // ORD 1: interior rows 1 .. SEG-2 first (their sums are all local), so the LDS
+            // reads land while they compute; window P, Q, R = sums of rows i-1, i, i+1
             uint32_t P[NS], Q[NS], S1[NS];
 #pragma unroll
             for (int k = 0; k < NS; ++k) P[k] = F[k];
@@ -236,6 +240,13 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
                 }
             }
             // (P = the sums of row SEG-2, or of row 0 when SEG == 2)
+            if constexpr (ORD == 2) {
+                // ORD 2: the barrier after the interior rows -- a wave that arrives early has
+                // already done all the work that needs no neighbour
+                __syncthreads();
+                get(xbot(p, s_up), has_up, U);
+                get(xtop(p, s_dn), has_dn, D);
+            }
             rule(U, F, S1, v[0]);
             rule(P, Lr, D, v[SEG - 1]);
         }

@@ -23,6 +23,7 @@ static void *tile_fn(int seg)
     case 32: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<32, ORD, 1>) : nullptr;
     case 40: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<40, ORD, 1>) : nullptr;
     case 48: return W == 1 && ORD == 0 ? reinterpret_cast<void *>(&k_step_tile<48, 0, 1>) : nullptr;
+    // (ORD 2 at SEG < 3 is ORD 1: no interior row)
     default: return nullptr;
     }
 }
@@ -30,9 +31,9 @@ static void *tile_fn(int seg)
 void *tile_kernel(int code)
 {
     const int seg = code % 100, ord = (code / 100) % 10, w = tile_seg_words(code);
-    if (code < 0 || ord > 1 || w > 2) return nullptr;
-    if (w == 2) return ord ? tile_fn<1, 2>(seg) : tile_fn<0, 2>(seg);
-    return ord ? tile_fn<1, 1>(seg) : tile_fn<0, 1>(seg);
+    if (code < 0 || ord > 2 || w > 2) return nullptr;
+    if (w == 2) return ord == 2 ? tile_fn<2, 2>(seg) : ord ? tile_fn<1, 2>(seg) : tile_fn<0, 2>(seg);
+    return ord == 2 ? tile_fn<2, 1>(seg) : ord ? tile_fn<1, 1>(seg) : tile_fn<0, 1>(seg);
 }
 
 bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)

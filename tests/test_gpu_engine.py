@@ -628,6 +628,10 @@ TILE_CASES = [
     (256, 3, 2, 1, 1002, 24, 30),         # 2 lane columns on a 3-row torus
     (384, 100, 3, 25, 1112, 12, 25),      # 3 lane columns: one tile, halo lanes wrap
     (65536, 96, 14, 24, 1016, 16, 33),    # the headline width, ORD 0 at SEG 16
+    # ORD 2: the barrier after the interior rows
+    (5120, 300, 10, 37, 206, 16, 40),
+    (8320, 41, 62, 13, 224, 20, 44),
+    (2048, 500, 14, 40, 1208, 16, 50),
 ]
 
 

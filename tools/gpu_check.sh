@@ -45,6 +45,7 @@ for step in "$@"; do
     sq65)   run sq65 300 bash tools/pmc_sq.sh ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
+    prof3)  run prof3 1000 bash tools/profile_r03.sh ;;
     bench20) run bench20 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     newt)   run newt 400 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "tile or small_board or rejects_tools or spin_timeout or snapshot_while or control_word or 5120 or random_vs_oracle" ;;
     c2tile) run c2tile 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --shapes 10:160:4:32,10:160:4:16,10:160:3:24,10:160:8:32,10:80:4:16,10:80:2:12,16:160:4:24,14:160:4:24,20:320:4:32,10:160:12:32,10:320:16:32,30:320:16:16,10:96:2:32,10:128:2:16,10:64:2:16,10:160:2:24,14:128:2:16,6:128:3:16,6:96:2:16 ;;
