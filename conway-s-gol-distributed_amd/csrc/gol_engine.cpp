@@ -585,9 +585,11 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     std::sort(wopt.begin(), wopt.end(), [](const WOpt &x, const WOpt &y) {
         return x.useful > y.useful || (x.useful == y.useful && x.tw > y.tw);
     });
-    std::vector<int> tws;
-    for (const WOpt &w : wopt)
+    std::vector<int> tws, tws_wide;                  // the 3 best-filled widths; 8 within 80 %
+    for (const WOpt &w : wopt) {
         if ((int)tws.size() < 3 && w.useful >= wopt[0].useful * 0.9) tws.push_back(w.tw);
+        if ((int)tws_wide.size() < 8 && w.useful >= wopt[0].useful * 0.8) tws_wide.push_back(w.tw);
+    }
     static const int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
                                  106, 108, 112, 116, 124, 132, 140,
                                  203, 204, 206, 208, 212, 216, 224, 232, 240};
@@ -696,6 +698,13 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     if (kfix <= 0) {
         const P base = cur;
         for (int K : {12, 16, 20, 24, 32}) improve(P{K, base.wv, base.tw, base.seg});
+    }
+    {
+        // width x waves jointly (the tile height follows both: 5120^2 ran best at 10 words x
+        // 12 waves, a width the fill ranking puts 4th, profiles/r03_tile_grid_5.log)
+        const P base = cur;
+        for (int tw : tws_wide)
+            for (int wv : {8, 12, 16}) improve(P{base.K, wv, tw, base.seg});
     }
     {
         const P base = cur;

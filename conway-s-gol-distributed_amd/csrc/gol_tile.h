@@ -177,12 +177,12 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
             put(xbot(p, slot), Lr);
         }
         uint32_t U[NS], D[NS];
-        if constexpr (ORD < 2) {
-            __syncthreads();
+        if constexpr (ORD < 2 || ORD == 3) {
+            if constexpr (ORD != 3) __syncthreads();   // ORD 3: timing ablation (tools build)
             get(xbot(p, s_up), has_up, U);
             get(xtop(p, s_dn), has_dn, D);
         }
-        if constexpr (ORD == 0) {
+        if constexpr (ORD == 0 || ORD == 3) {
             // in order: A, B, Cs = sums of rows i-1, i, i+1
             uint32_t A[NS], B[NS];
 #pragma unroll

@@ -45,6 +45,9 @@ for step in "$@"; do
     sq65)   run sq65 300 bash tools/pmc_sq.sh ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
+    nobar)  run nobar 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 5120 --turns 960 --rounds 3 --shapes 30:64:8:32,30:64:308:32,30:64:4:32,30:64:304:32,10:160:4:32,10:160:304:32 && run nobar16 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 16384 --turns 320 --rounds 3 --shapes 29:320:24:32,29:320:324:32 ;;
+    sqc2)   run sqc2 300 env TAG=_c2 bash tools/pmc_sq.sh tools/kernel_run.py --size 5120 --mv 15 --tpl 32 --band 160 --tile 10,4 --turns 3200 && run sqc3 300 env TAG=_c3 bash tools/pmc_sq.sh tools/kernel_run.py --size 16384 --mv 15 --tpl 32 --band 320 --tile 29,124 --turns 640 ;;
+    bench2g) run bench2g 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --backend gloo --c3-size 4096 --c3-turns 300 ;;
     prof3)  run prof3 1000 bash tools/profile_r03.sh ;;
     bench20) run bench20 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     newt)   run newt 400 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "tile or small_board or rejects_tools or spin_timeout or snapshot_while or control_word or 5120 or random_vs_oracle" ;;
