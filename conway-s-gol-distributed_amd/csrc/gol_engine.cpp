@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <iterator>
 #include <map>
 #include <tuple>
 #include <mutex>
@@ -593,8 +594,7 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     static const int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
                                  106, 108, 112, 116, 124, 132, 140,
                                  203, 204, 206, 208, 212, 216, 224, 232, 240};
-    static const int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1012, 1016,
-                                 1106, 1108, 1112, 1116, 1204, 1206, 1208, 1212, 1216};
+    static const int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1106, 1108, 1204, 1206, 1208};
     std::vector<int> segs = W == 1 ? std::vector<int>(std::begin(kSegs1), std::end(kSegs1))
                                    : std::vector<int>(std::begin(kSegs2), std::end(kSegs2));
     struct P { int K, wv, tw, seg, th = 0; };          // th > 0: this height (<= wv's)
@@ -683,6 +683,19 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
             cur = p;
         }
     };
+    if ((long long)nw * rows < (1ll << 23)) {
+        // boards up to 16384^2: SEG x width x waves jointly first (one turn order) -- one
+        // parameter at a time settled on 5120^2 at 18-word tiles of SEG 8 (0.76 us per turn)
+        // while 14 x 128 tiles of SEG 6 ran 0.64 (profiles/r03_tile_sweep_5120_v2.log)
+        static const int kJoint1[] = {102, 103, 104, 106, 108, 112, 116, 124};
+        static const int kJoint2[] = {1102, 1103, 1104, 1106, 1108};
+        const P base = cur;
+        const int *js = W == 1 ? kJoint1 : kJoint2;
+        const int nj = W == 1 ? (int)std::size(kJoint1) : (int)std::size(kJoint2);
+        for (int i = 0; i < nj; ++i)
+            for (int tw : tws_wide)
+                for (int wv : {8, 12, 16}) improve(P{base.K, wv, tw, js[i]});
+    }
     {
         const P base = cur;
         for (int sg : segs) improve(P{base.K, base.wv, base.tw, sg});

@@ -32,6 +32,8 @@
 #pragma once
 #include "gol_device.h"
 
+#include <type_traits>
+
 namespace golk {
 
 constexpr int kTileMaxWaves = 16;                       // 1024 threads per workgroup
@@ -148,39 +150,65 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
             base[(size_t)q * nslot * 4] =
                 make_uint4(S[4 * q], S[4 * q + 1], S[4 * q + 2], S[4 * q + 3]);
     };
-    auto get = [&](const uint4 *base, bool has, uint32_t (&S)[NS]) {
+    auto get = [&](const uint4 *base, uint32_t (&S)[NS]) {
 #pragma unroll
         for (int q = 0; q < W; ++q) {
             const uint4 u = base[(size_t)q * nslot * 4];
-            S[4 * q] = has ? u.x : 0u;
-            S[4 * q + 1] = has ? u.y : 0u;
-            S[4 * q + 2] = has ? u.z : 0u;
-            S[4 * q + 3] = has ? u.w : 0u;
+            S[4 * q] = u.x;
+            S[4 * q + 1] = u.y;
+            S[4 * q + 2] = u.z;
+            S[4 * q + 3] = u.w;
         }
     };
-    // slot arrays: [q][parity][top / bottom][slot], q = the word of the lane
-    auto xtop = [&](int p, int sl) { return xsh + (size_t)(p * 2 + 0) * nslot + sl; };
-    auto xbot = [&](int p, int sl) { return xsh + (size_t)(p * 2 + 1) * nslot + sl; };
-    const bool has_up = live && seg > 0, has_dn = live && seg + 1 < nseg;
-    // neighbour slots, clamped to a valid one where there is no neighbour (then masked to 0):
-    // the LDS reads stay unconditional, so no branch splits the turn's straight-line code
-    const int s_up = has_up ? slot - C : 0, s_dn = has_dn ? slot + C : 0;
-    for (int t = 0; t < K; ++t) {
-        const int p = t & 1;
+    // Slot arrays: [q][parity][top / bottom][slot], q = the word of the lane.  Every lane
+    // writes and reads every turn, with no mask: the idle lanes (group >= G) own the slots
+    // past the tile's (waves x G x C .. waves x 64), and a segment with no neighbour above
+    // (below) reads its own slot.  What it reads there is junk, but it only reaches the tile's
+    // outermost row, whose error moves inward one row per turn like that of any halo row.
+    const int nlive = (int)(blockDim.x >> 6) * G * C;
+    const int myslot = live ? slot : nlive + wave * (64 - G * C) + (lane - G * C);
+    const int s_up = live && seg > 0 ? slot - C : myslot;
+    const int s_dn = live && seg + 1 < nseg ? slot + C : myslot;
+    // the lane's four LDS slots at parity 0
+    // Turn parity p uses the slots 2 p nslot further on.  Short segments run two turns per
+    // loop iteration with p a compile-time constant (the parity's addresses hoisted out of the
+    // loop: 11 % faster turns at SEG 3-4); long ones one turn body with the offset added per
+    // turn -- the doubled body of a long segment ran 10-14 % slower (instruction fetch,
+    // profiles/r03_tile_unroll_ab.log).
+    constexpr bool kPairs = SEG * W <= 12;
+    // (with pairs the parity's four addresses are loop-invariant registers; one body forms
+    // them per turn -- precomputed, the long bodies ran 4-8 % slower)
+    uint4 *const wtop2[2] = {xsh + myslot, xsh + 2 * nslot + myslot};
+    uint4 *const wbot2[2] = {xsh + nslot + myslot, xsh + 3 * nslot + myslot};
+    const uint4 *const rup2[2] = {xsh + nslot + s_up, xsh + 3 * nslot + s_up};
+    const uint4 *const rdn2[2] = {xsh + s_dn, xsh + 2 * nslot + s_dn};
+    auto wtop = [&](int p, int off) { return kPairs ? wtop2[p] : xsh + off + myslot; };
+    auto wbot = [&](int p, int off) { return kPairs ? wbot2[p] : xsh + off + nslot + myslot; };
+    auto rup = [&](int p, int off) {
+        return kPairs ? rup2[p] : (const uint4 *)(xsh + off + nslot + s_up);
+    };
+    auto rdn = [&](int p, int off) { return kPairs ? rdn2[p] : (const uint4 *)(xsh + off + s_dn); };
+    // A wave whose rows are all outside the turn's trapezoid leaves: the tile's rows
+    // [t + 1, 2K + TH - 1 - t) change at turn t (t = 0 .. K-1) and need the sums of the rows
+    // one further out; a wave above row t (below row 2K + TH - 1 - t) holds no row that any
+    // later turn or the final store needs (its rows are < K, resp. >= K + TH), and the
+    // workgroup barrier no longer counts it once it has ended.
+    const int wrow0 = wave * G * SEG, wrow1 = wrow0 + G * SEG;  // the wave's tile rows
+    auto turn = [&](auto P, int poff) {
+        constexpr int p = decltype(P)::value;
+        const int off = poff;
         // the segment's first and last row sums go to the neighbours (row sums, not rows: no
         // lane sums a row twice -- SEG row sums and SEG rules per turn)
         uint32_t F[NS], Lr[NS];
         rsum(v[0], F);
         rsum(v[SEG - 1], Lr);
-        if (live) {
-            put(xtop(p, slot), F);
-            put(xbot(p, slot), Lr);
-        }
+        put(wtop(p, off), F);
+        put(wbot(p, off), Lr);
         uint32_t U[NS], D[NS];
         if constexpr (ORD < 2 || ORD == 3) {
             if constexpr (ORD != 3) __syncthreads();   // ORD 3: timing ablation (tools build)
-            get(xbot(p, s_up), has_up, U);
-            get(xtop(p, s_dn), has_dn, D);
+            get(rup(p, off), U);
+            get(rdn(p, off), D);
         }
         if constexpr (ORD == 0 || ORD == 3) {
             // in order: A, B, Cs = sums of rows i-1, i, i+1
@@ -212,9 +240,9 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
         } else {
             // ORD 1: interior rows 1 .. SEG-2 first (their sums are all local), so the LDS
             // reads land while they compute; window P, Q, R = sums of rows i-1, i, i+1
-            uint32_t P[NS], Q[NS], S1[NS];
+            uint32_t Pw[NS], Q[NS], S1[NS];
 #pragma unroll
-            for (int k = 0; k < NS; ++k) P[k] = F[k];
+            for (int k = 0; k < NS; ++k) Pw[k] = F[k];
             if constexpr (SEG >= 3) {
                 rsum(v[1], Q);
 #pragma unroll
@@ -232,23 +260,38 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
                 } else {
                     rsum(v[i + 1], R);
                 }
-                rule(P, Q, R, v[i]);
+                rule(Pw, Q, R, v[i]);
 #pragma unroll
                 for (int k = 0; k < NS; ++k) {
-                    P[k] = Q[k];
+                    Pw[k] = Q[k];
                     Q[k] = R[k];
                 }
             }
-            // (P = the sums of row SEG-2, or of row 0 when SEG == 2)
+            // (Pw = the sums of row SEG-2, or of row 0 when SEG == 2)
             if constexpr (ORD == 2) {
                 // ORD 2: the barrier after the interior rows -- a wave that arrives early has
                 // already done all the work that needs no neighbour
                 __syncthreads();
-                get(xbot(p, s_up), has_up, U);
-                get(xtop(p, s_dn), has_dn, D);
+                get(rup(p, off), U);
+                get(rdn(p, off), D);
             }
             rule(U, F, S1, v[0]);
-            rule(P, Lr, D, v[SEG - 1]);
+            rule(Pw, Lr, D, v[SEG - 1]);
+        }
+    };
+    const int lastrow = 2 * K + TH - 1;
+    if constexpr (!kPairs) {
+        for (int t = 0; t < K; ++t) {
+            if (wrow1 <= t || wrow0 > lastrow - t) return;   // (wave-uniform)
+            turn(std::integral_constant<int, 0>{}, (t & 1) * 2 * nslot);
+        }
+    } else {
+        for (int t = 0; t < K; t += 2) {
+            if (wrow1 <= t || wrow0 > lastrow - t) return;
+            turn(std::integral_constant<int, 0>{}, 0);
+            if (t + 1 == K) break;
+            if (wrow1 <= t + 1 || wrow0 > lastrow - t - 1) return;
+            turn(std::integral_constant<int, 1>{}, 0);
         }
     }
     // interior rows [K, K + TH) of the tile, below row_hi; interior columns inside the row

@@ -17,8 +17,9 @@ static void *tile_fn(int seg)
     case 4: return reinterpret_cast<void *>(&k_step_tile<4, ORD, W>);
     case 6: return reinterpret_cast<void *>(&k_step_tile<6, ORD, W>);
     case 8: return reinterpret_cast<void *>(&k_step_tile<8, ORD, W>);
-    case 12: return reinterpret_cast<void *>(&k_step_tile<12, ORD, W>);
-    case 16: return reinterpret_cast<void *>(&k_step_tile<16, ORD, W>);
+    // (two words per lane stop at SEG 8: deeper segments spill at the 128-VGPR cap)
+    case 12: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<12, ORD, 1>) : nullptr;
+    case 16: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<16, ORD, 1>) : nullptr;
     case 24: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<24, ORD, 1>) : nullptr;
     case 32: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<32, ORD, 1>) : nullptr;
     case 40: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<40, ORD, 1>) : nullptr;

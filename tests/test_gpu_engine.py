@@ -626,12 +626,18 @@ TILE_CASES = [
     (1024, 203, 7, 20, 1106, 8, 19),      # 8 lane columns: a partial last tile (1 lane)
     (8320, 41, 30, 13, 1008, 20, 44),     # 65 lane columns: partial, G = 2
     (256, 3, 2, 1, 1002, 24, 30),         # 2 lane columns on a 3-row torus
-    (384, 100, 3, 25, 1112, 12, 25),      # 3 lane columns: one tile, halo lanes wrap
-    (65536, 96, 14, 24, 1016, 16, 33),    # the headline width, ORD 0 at SEG 16
+    (384, 100, 3, 25, 1108, 12, 25),      # 3 lane columns: one tile, halo lanes wrap
+    (65536, 96, 14, 24, 1008, 16, 33),    # the headline width, ORD 0 at SEG 8
     # ORD 2: the barrier after the interior rows
     (5120, 300, 10, 37, 206, 16, 40),
     (8320, 41, 62, 13, 224, 20, 44),
     (2048, 500, 14, 40, 1208, 16, 50),
+    # waves that leave early: 8-row waves (G = 4, SEG 2) under 32 halo rows -- the top and
+    # bottom three waves end after 8 / 16 / 24 turns; and 16-row waves in the C2 shape
+    (2048, 500, 14, 40, 2, 32, 70),
+    (2048, 500, 14, 40, 102, 32, 70),
+    (5120, 5120, 30, 64, 8, 32, 70),
+    (5120, 5120, 30, 64, 208, 32, 70),
 ]
 
 

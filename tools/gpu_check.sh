@@ -59,6 +59,11 @@ for step in "$@"; do
     grid65) run grid65 500 python -u tools/tile_sweep.py --size 65536 --turns 64 --rounds 2 --grid 30,14,62/16,24,32,40,116,124,132,140/16,32/8 ;;
     bigtile) run bigtile 300 python -u tools/tile_sweep.py --size 16384 --turns 320 --shapes 30:586:40:32,30:586:48:32,62:512:40:32,62:400:32:32,14:900:16:24,30:300:24:16 ;;
     bigtile65) run bigtile65 300 python -u tools/tile_sweep.py --size 65536 --turns 64 --rounds 2 --shapes 62:576:40:32,30:576:40:32,62:448:32:32,14:900:16:24,62:700:48:16 ;;
+    tilesw5) run tilesw5 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --shapes 10:160:4:32,10:128:4:32,30:64:8:32,30:64:208:32,14:128:106:32,10:160:106:32,10:96:4:24 ;;
+    tilesw16) run tilesw16 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 16384 --auto --turns 960 --shapes 29:320:24:32,29:320:124:32,29:320:224:32 ;;
+    ab16) run ab16_old 200 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_old.so python -u tools/tile_sweep.py --size 16384 --turns 960 --shapes 29:320:24:32,29:320:124:32 && run ab16_new 200 python -u tools/tile_sweep.py --size 16384 --turns 960 --shapes 29:320:24:32,29:320:124:32 && run ab5_old 200 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_old.so python -u tools/tile_sweep.py --size 5120 --turns 960 --shapes 10:160:4:32,14:128:106:32 && run ab5_new 200 python -u tools/tile_sweep.py --size 5120 --turns 960 --shapes 10:160:4:32,14:128:106:32 ;;
+    abx) run abx16 500 env LIBS="old new exp2" bash tools/ab_tile.sh 16384 640 29:320:24:32,29:320:124:32,14:320:106:32 && run abx65 500 env LIBS="old new exp2" bash tools/ab_tile.sh 65536 64 30:576:40:32,30:576:140:32 && run abx5 300 env LIBS="old new exp2" bash tools/ab_tile.sh 5120 960 10:160:4:32,14:128:103:32 ;;
+    aby) run aby16 500 env LIBS="old new old new" bash tools/ab_tile.sh 16384 640 29:320:124:32,14:320:106:32 && run aby65 500 env LIBS="old new old new" bash tools/ab_tile.sh 65536 64 30:576:140:32 && run aby5 300 env LIBS="old new" bash tools/ab_tile.sh 5120 960 10:160:4:32,14:128:103:32 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done
