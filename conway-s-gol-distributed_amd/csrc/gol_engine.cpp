@@ -695,6 +695,14 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         for (int i = 0; i < nj; ++i)
             for (int tw : tws_wide)
                 for (int wv : {8, 12, 16}) improve(P{base.K, wv, tw, js[i]});
+    } else if (W == 1) {
+        // larger boards: the short-segment family on 14-word tiles (4 groups of 16 lanes, 16
+        // waves at <= 64 VGPRs: 8 waves per SIMD) -- 11 % faster than 62-word SEG 32 tiles on
+        // the 8-strip shape, 8 % slower at 65536^2 (profiles/r03_tile_small_seg_65536.log)
+        const P base = cur;
+        for (int sg : {104, 106, 206, 108})
+            for (int tw : {14, tws.empty() ? 14 : tws[0]})
+                for (int wv : {8, 16}) improve(P{base.K, wv, tw, sg});
     }
     {
         const P base = cur;

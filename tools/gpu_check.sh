@@ -64,6 +64,7 @@ for step in "$@"; do
     ab16) run ab16_old 200 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_old.so python -u tools/tile_sweep.py --size 16384 --turns 960 --shapes 29:320:24:32,29:320:124:32 && run ab16_new 200 python -u tools/tile_sweep.py --size 16384 --turns 960 --shapes 29:320:24:32,29:320:124:32 && run ab5_old 200 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_old.so python -u tools/tile_sweep.py --size 5120 --turns 960 --shapes 10:160:4:32,14:128:106:32 && run ab5_new 200 python -u tools/tile_sweep.py --size 5120 --turns 960 --shapes 10:160:4:32,14:128:106:32 ;;
     abx) run abx16 500 env LIBS="old new exp2" bash tools/ab_tile.sh 16384 640 29:320:24:32,29:320:124:32,14:320:106:32 && run abx65 500 env LIBS="old new exp2" bash tools/ab_tile.sh 65536 64 30:576:40:32,30:576:140:32 && run abx5 300 env LIBS="old new exp2" bash tools/ab_tile.sh 5120 960 10:160:4:32,14:128:103:32 ;;
     aby) run aby16 500 env LIBS="old new old new" bash tools/ab_tile.sh 16384 640 29:320:124:32,14:320:106:32 && run aby65 500 env LIBS="old new old new" bash tools/ab_tile.sh 65536 64 30:576:140:32 && run aby5 300 env LIBS="old new" bash tools/ab_tile.sh 5120 960 10:160:4:32,14:128:103:32 ;;
+    small65) run small65 400 python -u tools/tile_sweep.py --size 65536 --turns 96 --rounds 2 --shapes 30:576:140:32,14:320:106:32,14:352:106:16,14:336:106:24,14:352:206:16,14:224:104:16,14:352:6:16,10:256:104:32,10:288:104:16 && run small8448 400 python -u tools/tile_sweep.py --size 65536 --height 8448 --turns 192 --rounds 2 --shapes 62:192:132:32,14:320:106:32,14:352:106:16,14:336:106:24,14:352:206:16,14:224:104:16,14:352:6:16,10:288:104:16 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done
