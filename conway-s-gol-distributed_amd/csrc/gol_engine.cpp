@@ -753,11 +753,38 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
             }
         }
     }
+    // the search kept whatever beat the incumbent by 0.5 % on a best-of-2 timing; shapes
+    // within noise of each other can trade places from box to box, so the 4 fastest seen are
+    // timed again (best of 3) and the fastest of that final round is the pick
+    TileShape pick = best > 0.f ? shape(cur) : TileShape{};
+    if (pick.K) {
+        std::vector<std::pair<float, TileShape>> top;
+        for (const auto &m : memo)
+            if (m.second > 0.f)
+                top.push_back({m.second, TileShape{std::get<0>(m.first), std::get<1>(m.first),
+                                                   std::get<2>(m.first), std::get<3>(m.first), 0}});
+        std::sort(top.begin(), top.end(),
+                  [](const auto &x, const auto &y) { return x.first < y.first; });
+        if (top.size() > 4) top.resize(4);
+        float fbest = 0.f;
+        for (const auto &c2 : top) {
+            float v = 0.f;
+            for (int pass = 0; pass < 3; ++pass) {
+                const float u = time_one(c2.second, reps);
+                if (u > 0.f && (v == 0.f || u < v)) v = u;
+            }
+            if (v > 0.f && (fbest == 0.f || v < fbest)) {
+                fbest = v;
+                pick = c2.second;
+            }
+        }
+        if (fbest > 0.f) best = fbest;
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipGetLastError();
     *us = best * 1000.f;
-    return best > 0.f ? shape(cur) : TileShape{};
+    return pick;
 }
 
 // Boards below 2^20 words (5120^2: 409 600) cannot fill the GPU with band pipelines: they run
