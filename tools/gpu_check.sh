@@ -67,6 +67,8 @@ for step in "$@"; do
     small65) run small65 400 python -u tools/tile_sweep.py --size 65536 --turns 96 --rounds 2 --shapes 30:576:140:32,14:320:106:32,14:352:106:16,14:336:106:24,14:352:206:16,14:224:104:16,14:352:6:16,10:256:104:32,10:288:104:16 && run small8448 400 python -u tools/tile_sweep.py --size 65536 --height 8448 --turns 192 --rounds 2 --shapes 62:192:132:32,14:320:106:32,14:352:106:16,14:336:106:24,14:352:206:16,14:224:104:16,14:352:6:16,10:288:104:16 ;;
     sqb) run sqc2b 300 env TAG=_c2b bash tools/pmc_sq.sh tools/kernel_run.py --size 5120 --mv 15 --tpl 32 --band 128 --tile 14,103 --turns 3200 && run sqc3b 300 env TAG=_c3b bash tools/pmc_sq.sh tools/kernel_run.py --size 16384 --mv 15 --tpl 32 --band 320 --tile 14,106 --turns 640 ;;
     kfix) run kfix 300 python -u tools/tile_sweep.py --size 5120 --turns 960 --rounds 2 --shapes 14:128:104:2,14:128:104:4,14:128:104:8,14:128:104:16,14:128:104:32,14:128:103:32,14:128:103:16 && run kfix16 300 python -u tools/tile_sweep.py --size 16384 --turns 640 --rounds 2 --shapes 14:320:106:2,14:320:106:4,14:320:106:8,14:320:106:16,14:320:106:32 ;;
+    prof3b) run prof3b 800 bash tools/profile_r03b.sh ;;
+    prof3bk) run prof3bk 500 env ONLY_K20=1 bash tools/profile_r03b.sh ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done

@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 run of bench.py into profiles/<tag>_*.{csv,json}.
 
-Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD]
+Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL]
   SRC    the pass directory root (tools/profile_r02.sh: gpurun_out/prof2)
   KT     the --kernel-trace --stats pass (KT/ + KT.log holding the bench line), or - for
          a PMC-only summary
   FETCH / WRITE  the --pmc FETCH_SIZE / WRITE_SIZE passes of the same workload
   BOARD  which board of the bench run: 0 = the headline board, 1 = configs_measured[0]
+  KERNEL (PMC passes of tools/kernel_run.py, which loads no board): the last 20 dispatches
+         whose name contains this text instead of the first board's
 
 Timed dispatches: bench.py loads each board (k_il_convert), steps the warm-up turns, then
 the timed turns, so the timed launches are the last `launches` stencil dispatches
@@ -53,7 +55,7 @@ def load_rows(path):
     return rows
 
 
-def main(tag, src, kt, fetch=None, write=None, board="0"):
+def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None):
     board = int(board)
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -89,7 +91,10 @@ def main(tag, src, kt, fetch=None, write=None, board="0"):
             continue
         rows = [r for r in load_rows(os.path.join(src, name, "run_counter_collection.csv"))
                 if r["Counter_Name"] == counter]
-        seg = board_segments(rows)[0][-20:]
+        if kernel:
+            seg = [r for r in rows if kernel in r["Kernel_Name"]][-20:]
+        else:
+            seg = board_segments(rows)[0][-20:]
         res[counter + "_kernels"] = sorted({r["Kernel_Name"] for r in seg})
         res[counter + "_kib_median"] = statistics.median(float(r["Counter_Value"]) for r in seg)
         res[counter + "_launches"] = len(seg)
