@@ -69,6 +69,8 @@ for step in "$@"; do
     kfix) run kfix 300 python -u tools/tile_sweep.py --size 5120 --turns 960 --rounds 2 --shapes 14:128:104:2,14:128:104:4,14:128:104:8,14:128:104:16,14:128:104:32,14:128:103:32,14:128:103:16 && run kfix16 300 python -u tools/tile_sweep.py --size 16384 --turns 640 --rounds 2 --shapes 14:320:106:2,14:320:106:4,14:320:106:8,14:320:106:16,14:320:106:32 ;;
     prof3b) run prof3b 800 bash tools/profile_r03b.sh ;;
     prof3bk) run prof3bk 500 env ONLY_K20=1 bash tools/profile_r03b.sh ;;
+    k20) run k20 400 python -u tools/tile_sweep.py --size 65536 --turns 80 --rounds 3 --shapes 14:960:116:20,14:960:16:20,14:984:16:20,14:960:216:20,30:600:140:20,30:600:40:20,14:448:8:20,14:448:108:20,14:960:16:32,30:576:140:32 ;;
+    warm) for w in 5 60 5; do run warm$w 200 python -u bench.py --gpus 1 --steps 20 --warmup $w --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done; run warm40 200 python -u bench.py --gpus 1 --steps 40 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done
