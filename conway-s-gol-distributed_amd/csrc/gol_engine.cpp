@@ -686,7 +686,7 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     if ((long long)nw * rows < (1ll << 23)) {
         // boards up to 16384^2: SEG x width x waves jointly first (one turn order) -- one
         // parameter at a time settled on 5120^2 at 18-word tiles of SEG 8 (0.76 us per turn)
-        // while 14 x 128 tiles of SEG 6 ran 0.64 (profiles/r03_tile_sweep_5120_v2.log)
+        // while 14 x 128 tiles of SEG 6 ran 0.64 (profiles/r03b_tile_search_5120.log)
         static const int kJoint1[] = {102, 103, 104, 106, 108, 112, 116, 124};
         static const int kJoint2[] = {1102, 1103, 1104, 1106, 1108};
         const P base = cur;
