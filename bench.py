@@ -238,7 +238,7 @@ KERNELS = {7: "k_step_skew<K> (interleaved layout, one pipeline per wave)",
            12: "k_step_wg<K> (helix tiles, parallelogram bands)",
            13: "k_step_wg<K> (helix tiles, in-order stages)",
            14: "k_step_wg<K> (parallelogram bands, in-order stages)",
-           15: "k_step_tile<K> (2-D tile resident in registers, small boards)",
+           15: "k_step_tile<K> (2-D tile resident in registers for all K turns)",
            0: "k_step_ring<D=3> (one turn per launch)"}
 
 
