@@ -34,6 +34,10 @@
 
 #include <type_traits>
 
+#ifndef GOL_TILE_PAIRS_MAX   // (experiments: the longest segment that runs turns in pairs)
+#define GOL_TILE_PAIRS_MAX 12
+#endif
+
 namespace golk {
 
 constexpr int kTileMaxWaves = 16;                       // 1024 threads per workgroup
@@ -174,8 +178,9 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
     // loop iteration with p a compile-time constant (the parity's addresses hoisted out of the
     // loop: 11 % faster turns at SEG 3-4); long ones one turn body with the offset added per
     // turn -- the doubled body of a long segment ran 10-14 % slower (instruction fetch,
-    // profiles/r03_tile_unroll_ab.log).
-    constexpr bool kPairs = SEG * W <= 12;
+    // profiles/r03_tile_unroll_ab.log).  The threshold 12: pairs at SEG 8 are 2-3 % faster
+    // than one body, at SEG 16 11-28 % slower (profiles/r03b_tile_pairs_threshold.log).
+    constexpr bool kPairs = SEG * W <= GOL_TILE_PAIRS_MAX;
     // (with pairs the parity's four addresses are loop-invariant registers; one body forms
     // them per turn -- precomputed, the long bodies ran 4-8 % slower)
     uint4 *const wtop2[2] = {xsh + myslot, xsh + 2 * nslot + myslot};
