@@ -75,6 +75,7 @@ for step in "$@"; do
     pairs) run pairs16 400 env LIBS="new p7 p16 new" bash tools/ab_tile.sh 16384 640 14:448:208:32,14:448:108:32,14:704:112:32,14:960:116:32 && run pairs65 500 env LIBS="new p7 p16" bash tools/ab_tile.sh 65536 80 14:960:116:20,14:448:108:32 ;;
     cold) run coldt 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "planner or interleaved or control_word or snapshot" && run coldb 300 env GOL_AUTOTUNE_LOG=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 && run coldb2 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 ;;
     pin) for i in 1 2; do run pind$i 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 && run pin7_$i 300 env GOL_MULTI_VARIANT=7 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;
+    cold2) run coldt 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "planner or interleaved or control_word or snapshot" && for i in 1 2 3; do run coldb$i 300 env GOL_AUTOTUNE_LOG=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done
