@@ -76,10 +76,6 @@ struct gol_ctx {
     // launch planner (autotuned engines): plan[t] = the first launch of the fastest measured
     // sequence of launches for t turns (t <= kPlanMax; k = 0: no plan, use the even split)
     std::vector<Launch> plan;
-    // plan_cold[t]: the first launch of a gol_step call of t turns when the GPU starts it idle
-    // (each kernel family's single cold launch measured at create time; the rest of the call
-    // follows `plan`)
-    std::vector<Launch> plan_cold;
     std::vector<Launch> last;                // launches of the last gol_step (gol_last_launches)
     long long last_n = 0;
     int ncu = 0;                             // compute units of the device
@@ -193,7 +189,7 @@ struct TuneKey {
 struct TuneVal {
     int var, tpl, band, tile_w, tile_seg;
     float us;
-    std::vector<Launch> plan, plan_cold;
+    std::vector<Launch> plan;
 };
 std::mutex g_tune_mu;
 std::map<TuneKey, TuneVal> g_tune;
@@ -382,7 +378,7 @@ int band_for_depth(gol_ctx *c, int k)
 // gol_step and gol_halo_buffers both use this rule (the zero-copy halo layout must be the
 // layout the first launch after an exchange runs on; every planned kernel runs on the
 // interleaved layout).
-Launch plan_launch(gol_ctx *c, int64_t room, bool first)
+Launch plan_launch(gol_ctx *c, int64_t room)
 {
     Launch L{1, c->multi_variant, c->band};
     if (c->tpl <= 1 || room < 2 || (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) ||
@@ -390,8 +386,6 @@ Launch plan_launch(gol_ctx *c, int64_t room, bool first)
         return L;
     if (!c->plan.empty()) {
         if (room > kPlanMax) return Launch{c->tpl, c->multi_variant, c->band_multi};
-        if (first && !c->plan_cold.empty() && c->plan_cold[room].k >= 2)
-            return c->plan_cold[room];
         if (c->plan[room].k >= 2) return c->plan[room];
     }
     const int64_t nl = (room + c->tpl - 1) / c->tpl;
@@ -400,7 +394,7 @@ Launch plan_launch(gol_ctx *c, int64_t room, bool first)
     return Launch{k, c->multi_variant, band_for_depth(c, k)};
 }
 
-int launch_depth(gol_ctx *c, int64_t room) { return plan_launch(c, room, false).k; }
+int launch_depth(gol_ctx *c, int64_t room) { return plan_launch(c, room).k; }
 
 // the word layout a launch of depth k runs on
 bool stepping_il(const gol_ctx *c, int k)
@@ -566,7 +560,6 @@ void apply_tile(gol_ctx *c, const TileShape &t)
     c->tile_seg = t.seg;
     for (int &b : c->band_at) b = 0;
     c->plan.clear();
-    c->plan_cold.clear();
 }
 
 // Measured search for the k_step_tile shape (coordinate descent over the launch parameters;
@@ -1038,47 +1031,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                         plan[r] = Launch{k, f.var, f.band_k[k]};
                     }
                 }
-        // A gol_step call often starts on an idle GPU (a host that syncs between calls, the
-        // bench's timed region): its first launch then also pays the host's launch latency
-        // and the grid's ramp, which differ by kernel (65536^2, 20 turns: one k_step_tile
-        // launch +44 us over its back-to-back time, k_step_skew +16-19 us per launch).  Time
-        // one cold launch per family at its tuned depth (best of 3) and choose each call's
-        // first launch with that extra cost; the rest of the call follows the plan above.
-        std::vector<float> cold(fams.size(), 0.f);
-        for (size_t i = 0; i < fams.size(); ++i) {
-            const Fam &f = fams[i];
-            if (f.K < 2 || f.T[f.K] <= 0.f) continue;
-            float best1 = 0.f;
-            for (int pass = 0; pass < 3; ++pass) {
-                (void)hipStreamSynchronize(c->stream);
-                const float v = time_one(Cand{f.var, f.K, f.band_k[f.K], f.tw, f.seg}, 1) * f.K;
-                if (v > 0.f && (best1 == 0.f || v < best1)) best1 = v;
-            }
-            if (best1 > 0.f) cold[i] = std::max(0.f, best1 - f.T[f.K]);
-        }
-        std::vector<Launch> plan_cold(kPlanMax + 1, Launch{});
-        for (int r = 2; r <= kPlanMax; ++r) {
-            float bestc = inf;
-            for (size_t i = 0; i < fams.size(); ++i)
-                for (int k = 2; k <= std::min(r, golk::kMaxTurnsPerLaunch); ++k) {
-                    const Fam &f = fams[i];
-                    if (f.T[k] <= 0.f || r - k == 1 || cost[r - k] >= inf) continue;
-                    const float v = cost[r - k] + f.T[k] + cold[i];
-                    if (v < bestc) {
-                        bestc = v;
-                        plan_cold[r] = Launch{k, f.var, f.band_k[k]};
-                    }
-                }
-        }
-        c->plan_cold = std::move(plan_cold);
         if (getenv("GOL_AUTOTUNE_LOG")) {
-            for (size_t i = 0; i < fams.size(); ++i)
-                fprintf(stderr, "autotune cold launch var=%d K=%d extra_us=%.1f\n", fams[i].var,
-                        fams[i].K, cold[i] * 1000.f);
-            for (int r : {8, 16, 20, 32})
-                if (r <= kPlanMax && c->plan_cold[r].k >= 2)
-                    fprintf(stderr, "autotune cold plan %d turns: first %d(var %d, band %d)\n", r,
-                            c->plan_cold[r].k, c->plan_cold[r].var, c->plan_cold[r].band);
             for (const Fam &f : fams)
                 for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k)
                     if (f.T[k] > 0.f)
@@ -1316,7 +1269,6 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
             c->tile_w = v.tile_w;
             c->tile_seg = v.tile_seg;
             c->plan = v.plan;
-            c->plan_cold = v.plan_cold;
             c->tuned_us_per_turn = v.us;
             for (int &b : c->band_at) b = 0;
             cached = true;
@@ -1331,7 +1283,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         if (use_cache) {
             std::lock_guard<std::mutex> lk(g_tune_mu);
             g_tune[key] = TuneVal{c->multi_variant, c->tpl, c->band_multi, c->tile_w,
-                                  c->tile_seg, c->tuned_us_per_turn, c->plan, c->plan_cold};
+                                  c->tile_seg, c->tuned_us_per_turn, c->plan};
         }
     }
     if ((e = hipMemsetAsync(c->board[0], 0, words * 8, c->stream)) != hipSuccess ||
@@ -1652,8 +1604,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
         }
         int64_t room = turns - t;
         if (is_strip(c)) room = std::min<int64_t>(room, c->halo_valid);
-        // (the first launch of a torus engine's call may start on an idle GPU: plan_cold)
-        const Launch plan = plan_launch(c, room, t == 0 && !is_strip(c));
+        const Launch plan = plan_launch(c, room);
         const int k = plan.k;
         // rows computed: torus -> all; strip -> [s, buf_rows - s) after turn s since exchange
         const int s0 = is_strip(c) ? c->cfg.halo - c->halo_valid : 0;
