@@ -76,6 +76,7 @@ for step in "$@"; do
     cold) run coldt 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "planner or interleaved or control_word or snapshot" && run coldb 300 env GOL_AUTOTUNE_LOG=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 && run coldb2 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 ;;
     pin) for i in 1 2; do run pind$i 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 && run pin7_$i 300 env GOL_MULTI_VARIANT=7 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;
     cold2) run coldt 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "planner or interleaved or control_word or snapshot" && for i in 1 2 3; do run coldb$i 300 env GOL_AUTOTUNE_LOG=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;
+    c2b) run c2b 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --shapes 14:128:104:32,14:122:104:32,14:128:103:32,14:122:103:32 && run c2bench 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --no-c1 ;;
     sweep16k) run sweep16k 300 python -u tools/sweep.py --size 16384 --turns 1000 --variants 1,2,4,5 --bands 8,12,16,24 ;;
   esac
 done
