@@ -173,7 +173,6 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
     const int myslot = live ? slot : nlive + wave * (64 - G * C) + (lane - G * C);
     const int s_up = live && seg > 0 ? slot - C : myslot;
     const int s_dn = live && seg + 1 < nseg ? slot + C : myslot;
-    // the lane's four LDS slots at parity 0
     // Turn parity p uses the slots 2 p nslot further on.  Short segments run two turns per
     // loop iteration with p a compile-time constant (the parity's addresses hoisted out of the
     // loop: 11 % faster turns at SEG 3-4); long ones one turn body with the offset added per
@@ -181,8 +180,8 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
     // profiles/r03_tile_unroll_ab.log).  The threshold 12: pairs at SEG 8 are 2-3 % faster
     // than one body, at SEG 16 11-28 % slower (profiles/r03b_tile_pairs_threshold.log).
     constexpr bool kPairs = SEG * W <= GOL_TILE_PAIRS_MAX;
-    // (with pairs the parity's four addresses are loop-invariant registers; one body forms
-    // them per turn -- precomputed, the long bodies ran 4-8 % slower)
+    // (with pairs the lane's four LDS addresses of each parity are loop-invariant registers;
+    // one body forms them per turn -- precomputed there, the long bodies ran 4-8 % slower)
     uint4 *const wtop2[2] = {xsh + myslot, xsh + 2 * nslot + myslot};
     uint4 *const wbot2[2] = {xsh + nslot + myslot, xsh + 3 * nslot + myslot};
     const uint4 *const rup2[2] = {xsh + nslot + s_up, xsh + 3 * nslot + s_up};
