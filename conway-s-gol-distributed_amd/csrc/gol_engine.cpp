@@ -46,9 +46,12 @@ constexpr size_t kStagingBytes = 256u << 20;  // byte staging chunk for load / r
 
 }  // namespace
 
-// one temporal-blocking launch: depth, kernel (golk::kMulti*), band
+// one temporal-blocking launch: depth, kernel (golk::kMulti*), band, and for k_step_tile the
+// tile width and segment code it was timed at (a plan may hold a tile family other than the
+// engine's own pick: each launch carries its shape)
 struct Launch {
     int k = 0, var = 0, band = 0;
+    int tw = 0, seg = 0;
 };
 constexpr int kPlanMax = 128;               // launch plans cover gol_step / halo windows up to this
 constexpr size_t kLastCap = 4096;           // gol_last_launches records at most this many
@@ -380,18 +383,19 @@ int band_for_depth(gol_ctx *c, int k)
 // interleaved layout).
 Launch plan_launch(gol_ctx *c, int64_t room)
 {
-    Launch L{1, c->multi_variant, c->band};
+    Launch L{1, c->multi_variant, c->band, 0, 0};
     if (c->tpl <= 1 || room < 2 || (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) ||
         c->blocked_pending)
         return L;
     if (!c->plan.empty()) {
-        if (room > kPlanMax) return Launch{c->tpl, c->multi_variant, c->band_multi};
+        if (room > kPlanMax)
+            return Launch{c->tpl, c->multi_variant, c->band_multi, c->tile_w, c->tile_seg};
         if (c->plan[room].k >= 2) return c->plan[room];
     }
     const int64_t nl = (room + c->tpl - 1) / c->tpl;
     const int k = (int)((room + nl - 1) / nl);
     if (!golk::multi_ok(c->cfg.width, k, c->multi_variant)) return L;
-    return Launch{k, c->multi_variant, band_for_depth(c, k)};
+    return Launch{k, c->multi_variant, band_for_depth(c, k), c->tile_w, c->tile_seg};
 }
 
 int launch_depth(gol_ctx *c, int64_t room) { return plan_launch(c, room).k; }
@@ -467,6 +471,15 @@ static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
 }
 
 // ---------------------------------------------------------------- k_step_tile planning
+// every segment code a search below can pick is one the product ships (and tests)
+template <size_t N>
+constexpr bool all_shipped(const int (&codes)[N])
+{
+    for (int c : codes)
+        if (!golk::tile_code_shipped(c)) return false;
+    return true;
+}
+
 struct TileShape {
     int K = 0, th = 0, tw = 0, seg = 0;
     double model_us = 0;                     // modelled time per turn
@@ -505,8 +518,9 @@ double tile_model_us(int ncu, int nw, int rows, int K, int th, int tw, int seg)
 std::vector<TileShape> tile_candidates(int ncu, int nw, int rows, int keep)
 {
     // SEG, and SEG + 100 for the interior-rows-first turn order (gol_tile.hip)
-    static const int kSegs[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
-                                106, 108, 112, 116, 124, 132, 140};
+    static constexpr int kSegs[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
+                                    106, 108, 112, 116, 124, 132, 140};
+    static_assert(all_shipped(kSegs), "a tile code outside golk::kTileCodes");
     std::vector<TileShape> all;
     std::vector<int> tws;
     for (int ntx = 1; ntx <= nw; ++ntx) {
@@ -591,10 +605,11 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         if ((int)tws.size() < 3 && w.useful >= wopt[0].useful * 0.9) tws.push_back(w.tw);
         if ((int)tws_wide.size() < 8 && w.useful >= wopt[0].useful * 0.8) tws_wide.push_back(w.tw);
     }
-    static const int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
-                                 106, 108, 112, 116, 124, 132, 140,
-                                 203, 204, 206, 208, 212, 216, 224, 232, 240};
-    static const int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1106, 1108, 1204, 1206, 1208};
+    static constexpr int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
+                                     106, 108, 112, 116, 124, 132, 140,
+                                     203, 204, 206, 208, 212, 216, 224, 232, 240};
+    static constexpr int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1106, 1108, 1204, 1206, 1208};
+    static_assert(all_shipped(kSegs1) && all_shipped(kSegs2), "a tile code outside kTileCodes");
     std::vector<int> segs = W == 1 ? std::vector<int>(std::begin(kSegs1), std::end(kSegs1))
                                    : std::vector<int>(std::begin(kSegs2), std::end(kSegs2));
     struct P { int K, wv, tw, seg, th = 0; };          // th > 0: this height (<= wv's)
@@ -687,8 +702,9 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         // boards up to 16384^2: SEG x width x waves jointly first (one turn order) -- one
         // parameter at a time settled on 5120^2 at 18-word tiles of SEG 8 (0.76 us per turn)
         // while 14 x 128 tiles of SEG 6 ran 0.64 (profiles/r03b_tile_search_5120.log)
-        static const int kJoint1[] = {102, 103, 104, 106, 108, 112, 116, 124};
-        static const int kJoint2[] = {1102, 1103, 1104, 1106, 1108};
+        static constexpr int kJoint1[] = {102, 103, 104, 106, 108, 112, 116, 124};
+        static constexpr int kJoint2[] = {1102, 1103, 1104, 1106, 1108};
+        static_assert(all_shipped(kJoint1) && all_shipped(kJoint2), "tile code outside kTileCodes");
         const P base = cur;
         const int *js = W == 1 ? kJoint1 : kJoint2;
         const int nj = W == 1 ? (int)std::size(kJoint1) : (int)std::size(kJoint2);
@@ -700,7 +716,9 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         // waves at <= 64 VGPRs: 8 waves per SIMD) -- 11 % faster than 62-word SEG 32 tiles on
         // the 8-strip shape, 8 % slower at 65536^2 (profiles/r03_tile_small_seg_65536.log)
         const P base = cur;
-        for (int sg : {104, 106, 206, 108})
+        static constexpr int kShort[] = {104, 106, 206, 108};
+        static_assert(all_shipped(kShort), "a tile code outside kTileCodes");
+        for (int sg : kShort)
             for (int tw : {14, tws.empty() ? 14 : tws[0]})
                 for (int wv : {8, 16}) improve(P{base.K, wv, tw, sg});
     }
@@ -996,10 +1014,6 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                 if (cand[i].var == var && t[i] > 0.f && (bi < 0 || t[i] < t[bi])) bi = (int)i;
             if (bi < 0 || !golk::multi_is_il(c->multi_words, var)) continue;
             Fam f{var, cand[bi].K, cand[bi].band, cand[bi].tw, cand[bi].seg, {}, {}};
-            if (var == golk::kMultiTile) {       // (one tile shape per engine: this one)
-                c->tile_w = f.tw;
-                c->tile_seg = f.seg;
-            }
             for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k) {
                 f.T[k] = 0.f;
                 f.band_k[k] = 0;
@@ -1028,7 +1042,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                     const float v = cost[r - k] + f.T[k];
                     if (v < cost[r]) {
                         cost[r] = v;
-                        plan[r] = Launch{k, f.var, f.band_k[k]};
+                        plan[r] = Launch{k, f.var, f.band_k[k], f.tw, f.seg};
                     }
                 }
         if (getenv("GOL_AUTOTUNE_LOG")) {
@@ -1576,6 +1590,9 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
         }
     } ring;
     const bool ctl = c->control_used.load();
+    // a reader served during an earlier step does not shorten this one's queue: the bound
+    // comes back when a reader is served during this step (a ticker's snapshot)
+    c->readers.store(false);
     c->last.clear();
     c->last_n = 0;
     for (int64_t t = 0; t < turns;) {
@@ -1639,6 +1656,10 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
             a.counts = nullptr;
             a.band = plan.band;
             a.multi_variant = plan.var;
+            if (plan.var == golk::kMultiTile) {
+                a.tile_w = plan.tw;
+                a.tile_seg = plan.seg;
+            }
 #if GOL_TOOLS
             if (c->multi_variant == golk::kMultiWgDiag && !split) {
                 if (int rc = wg_diag_launch(c, a, k)) return rc;
@@ -1666,6 +1687,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
             }
             a.band = c->band;
             a.multi_variant = c->multi_variant;
+            a.tile_w = c->tile_w;
+            a.tile_seg = c->tile_seg;
         } else if (split) {
             // one-turn launches: interior now, the 2 x (halo) boundary rows after the receives
             a.blocked = c->blocked_pending ? c->blocked : nullptr;
@@ -1710,7 +1733,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
         c->progress.store(c->turn);
         c->launches += 1;
         if (c->last.size() < kLastCap)
-            c->last.push_back(k > 1 ? Launch{k, plan.var, plan.band} : Launch{1, 0, c->band});
+            c->last.push_back(k > 1 ? plan : Launch{1, 0, c->band, 0, 0});
         ++c->last_n;
         t += k;
         if (is_strip(c)) c->halo_valid -= k;
@@ -1759,6 +1782,30 @@ int gol_last_launches(gol_ctx *c, int32_t *turns, int32_t *kernel, int32_t *band
         band[i] = c->last[i].band;
     }
     return (int)std::min<long long>(c->last_n, 0x7fffffff);
+}
+
+int gol_last_launch_tiles(gol_ctx *c, int32_t *tile_w, int32_t *tile_seg, int32_t *waves,
+                          int32_t cap)
+{
+    if (!c || cap < 0 || (cap > 0 && (!tile_w || !tile_seg || !waves))) return GOL_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    const int n = (int)std::min<size_t>((size_t)cap, c->last.size());
+    for (int i = 0; i < n; ++i) {
+        const Launch &L = c->last[i];
+        const bool t = L.k > 1 && L.var == golk::kMultiTile;
+        tile_w[i] = t ? L.tw : 0;
+        tile_seg[i] = t ? L.seg : 0;
+        waves[i] = t ? golk::tile_waves(L.k, L.band, L.tw, L.seg) : 0;
+    }
+    return (int)std::min<long long>(c->last_n, 0x7fffffff);
+}
+
+int gol_tile_codes(int32_t *codes, int32_t cap)
+{
+    const int n = (int)std::size(golk::kTileCodes);
+    if (cap < 0 || (cap > 0 && !codes)) return GOL_EINVAL;
+    for (int i = 0; i < std::min(n, (int)cap); ++i) codes[i] = golk::kTileCodes[i];
+    return n;
 }
 
 int gol_step_overlap(gol_ctx *c, int64_t turns, void *recv_stream)

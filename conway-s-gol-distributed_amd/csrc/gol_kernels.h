@@ -182,6 +182,25 @@ hipError_t launch_step_multi(const StepArgs &a, int turns, hipStream_t s);
 // k_step_tile (gol_tile.hip): a launch of `turns` turns on tiles of band x tile_w words with
 // tile_seg rows per lane; shape check, workgroup waves, tile count
 constexpr int kTileMaxWavesHost = 16;  // k_step_tile: waves per workgroup (gol_tile.h)
+// The k_step_tile segment codes (SEG + 100 * ORD + 1000 * (W - 1), gol_tile.h) the product
+// library runs: every code the engine's shape searches can pick (tile_candidates, tile_search)
+// and nothing else.  Each one is pinned by its own oracle parity test
+// (tests/test_gpu_engine.py::test_tile_code_pinned, read through gol_tile_codes), and
+// tile_shape_ok rejects the others outside the tools build.
+constexpr int kTileCodes[] = {
+    2,    3,    4,    6,    8,    12,   16,   24,   32,   40,   48,             // ORD 0, W 1
+    102,  103,  104,  106,  108,  112,  116,  124,  132,  140,                  // ORD 1
+    203,  204,  206,  208,  212,  216,  224,  232,  240,                        // ORD 2
+    1002, 1003, 1004, 1006, 1008,                                               // W 2
+    1102, 1103, 1104, 1106, 1108,
+    1204, 1206, 1208,
+};
+constexpr bool tile_code_shipped(int code)
+{
+    for (int c : kTileCodes)
+        if (c == code) return true;
+    return false;
+}
 bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg);
 int tile_waves(int turns, int tile_h, int tile_w, int seg);
 // resident workgroups per CU of that launch (occupancy API: VGPRs, LDS; 0 on error)

@@ -44,6 +44,7 @@ bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
 {
     if (turns < 2 || turns > 64 || tile_h < 1 || tile_w < 1 || tile_w + 2 > 64 || !tile_kernel(seg))
         return false;
+    if (!GOL_TOOLS && !tile_code_shipped(seg)) return false;   // (untested instantiations)
     if (nw % tile_seg_words(seg)) return false;          // (whole word pairs per lane)
     const int C = tile_w + 2, G = 64 / C;
     seg %= 100;

@@ -129,6 +129,13 @@ class Engine:
         n = self._c(self._L.gol_last_launches(self._h, *arrs, int(cap)))
         return [(arrs[0][i], arrs[1][i], arrs[2][i]) for i in range(min(n, cap))]
 
+    def last_launch_tiles(self, cap: int = 4096):
+        """[(tile width, segment code, waves per workgroup)] of the same launches (k_step_tile;
+        zeros for the other kernels)."""
+        arrs = [(ctypes.c_int32 * cap)() for _ in range(3)]
+        n = self._c(self._L.gol_last_launch_tiles(self._h, *arrs, int(cap)))
+        return [(arrs[0][i], arrs[1][i], arrs[2][i]) for i in range(min(n, cap))]
+
     # -- overlapped halo exchange (gol_stream_wait / gol_step_overlap)
     def stream_wait(self, stream_ptr: int):
         """Make `stream_ptr` wait for the work queued on the engine so far."""

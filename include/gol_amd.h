@@ -160,6 +160,15 @@ int gol_set_control(gol_ctx *ctx, int32_t word);
  * band rows.  Returns the number of launches (may exceed cap; entries past 4096 are not
  * recorded), or a negative GOL_E* code. */
 int gol_last_launches(gol_ctx *ctx, int32_t *turns, int32_t *kernel, int32_t *band, int32_t cap);
+/* The same launches' k_step_tile shapes (kernel 15): tile width in lanes, the segment code
+ * (SEG + 100 * turn order + 1000 * (words per lane - 1)) and the waves per workgroup; 0 for
+ * the other kernels.  Returns the launch count like gol_last_launches. */
+int gol_last_launch_tiles(gol_ctx *ctx, int32_t *tile_w, int32_t *tile_seg, int32_t *waves,
+                          int32_t cap);
+/* The k_step_tile segment codes this library runs (planner introspection for the parity
+ * tests: every code the shape search can pick has an oracle test).  Writes min(n, cap) codes,
+ * returns n.  Needs no device. */
+int gol_tile_codes(int32_t *codes, int32_t cap);
 /* Lock-free progress read for a controlling thread: *turn = turns enqueued so far (the
  * board reaches it at the next gol_sync), *parked = 1 while gol_step is parked on PAUSE
  * (the board is then complete at *turn).  Either pointer may be NULL. */

@@ -17,6 +17,18 @@ TOOLS_LIB = os.environ.get("GOL_AMD_LIB", "").endswith("libgolamd_tools.so")
 tools_only = pytest.mark.skipif(not TOOLS_LIB, reason="tools-build kernel (GOL_AMD_LIB=libgolamd_tools.so)")
 
 
+# The k_step_tile segment codes the product library runs (golk::kTileCodes, reported by
+# gol_tile_codes): SEG + 100 * turn order + 1000 * (words per lane - 1).  Each one has its own
+# oracle parity test (test_gpu_engine.py::test_tile_code_pinned); test_abi.py checks that the
+# library's list is this one, so a code added to the engine without a test fails on the CPU.
+TILE_CODES = (2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
+              102, 103, 104, 106, 108, 112, 116, 124, 132, 140,
+              203, 204, 206, 208, 212, 216, 224, 232, 240,
+              1002, 1003, 1004, 1006, 1008,
+              1102, 1103, 1104, 1106, 1108,
+              1204, 1206, 1208)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
 

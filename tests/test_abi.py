@@ -21,6 +21,19 @@ def test_header_symbols_exported():
     assert set(declared) <= exported
 
 
+def test_tile_codes_are_the_pinned_list():
+    """Every k_step_tile instantiation the product can run (gol_tile_codes; needs no device)
+    is one that test_gpu_engine.py::test_tile_code_pinned checks against the oracle."""
+    import ctypes as C
+    from conftest import TILE_CODES
+    from gol import _native as N
+    L = N.lib()
+    n = L.gol_tile_codes(None, 0)
+    buf = (C.c_int32 * n)()
+    assert L.gol_tile_codes(buf, n) == n
+    assert tuple(buf) == TILE_CODES
+
+
 def test_lib_is_gfx950_code_object():
     """The fat binary embeds a gfx950 (MI355X) code object."""
     from gol import _native as N

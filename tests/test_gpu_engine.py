@@ -511,6 +511,29 @@ def test_large_board_digests(gol, key):
         assert hashlib.sha256(words.tobytes()).hexdigest() == d["sha256"]
 
 
+@pytest.mark.parametrize("pin", [None, "tile"])
+def test_driver_command_digest(gol, monkeypatch, pin):
+    """The driver's bench command at the headline size (bench.py --steps 20 --warmup 5):
+    65536^2 seed 3, one gol_step of 5 turns, then one of 20, against the oracle digest of 25
+    turns -- with the plan the engine tunes for itself, and with the 20-turn launch pinned to
+    the k_step_tile shape the bench profiles (Measurement)."""
+    if pin == "tile":
+        monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+        monkeypatch.setenv("GOL_TILE", "14,116")
+        kw = dict(band_rows=960, turns_per_launch=20)
+    else:
+        kw = {}
+    d = _digests()["65536x65536_seed3_t25"]
+    with _engine(gol, d["width"], d["height"], **kw) as e:
+        e.fill_random(d["seed"])
+        e.step(5)
+        e.step(20)
+        if pin == "tile":
+            assert [(k, v) for k, v, _ in e.last_launches()] == [(20, 15)]
+        assert e.snapshot() == (25, d["alive"])
+        assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
+
+
 def test_65536_properties(gol, oracle):
     """Size-independent checks at the headline size: torus translation invariance
     (rolling the input by whole words commutes with the update) and 1-turn oracle parity."""
@@ -662,6 +685,53 @@ def test_tile_kernel(gol, oracle, monkeypatch, w, h, tw, th, seg, K, turns):
     want_mid = oracle.bit_run(start, w, turns)
     assert np.array_equal(mid, want_mid)
     assert np.array_equal(got, oracle.bit_run(want_mid, w, turns + 1))
+
+
+def _pinned_shape(code):
+    """A ragged k_step_tile shape for one segment code on the 4224 x 157 board of
+    test_tile_code_pinned: tile width (lanes) with several tiles per row and a partial last
+    one, tile height 100 (157 = 100 + 57), and more than one wave per workgroup."""
+    seg, words = code % 100, code // 1000 + 1
+    if words == 2:
+        return 7, 100          # 33 lane columns = 4 x 7 + 5; C = 9, G = 7
+    return (14, 100) if seg <= 8 else (30, 100)   # 66 words = 4 x 14 + 10 = 2 x 30 + 6
+
+
+@pytest.mark.parametrize("code", __import__("conftest").TILE_CODES)
+def test_tile_code_pinned(gol, oracle, monkeypatch, code):
+    """Every k_step_tile instantiation the product library can run (gol_tile_codes; the shape
+    searches pick only these) against the oracle: ragged tiles in both directions, one launch
+    of even depth (8) then launches of 8 and 7 turns (an odd depth ends a paired turn loop on
+    a single turn), 23 turns in all."""
+    tw, th = _pinned_shape(code)
+    w, h, K = 4224, 157, 8
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+    monkeypatch.setenv("GOL_TILE", f"{tw},{code}")
+    start = oracle.gen_random(code + 7, w, h)
+    with _engine(gol, w, h, band_rows=th, turns_per_launch=K) as e:
+        e.load_packed(start)
+        e.step(K)
+        assert [x[0] for x in e.last_launches()] == [K]
+        e.step(2 * K - 1)
+        assert sorted(x[0] for x in e.last_launches()) == [K - 1, K]
+        assert all(t == (tw, code) for t in
+                   [(a, b) for a, b, _ in e.last_launch_tiles()])
+        assert all(v > 1 for _, _, v in e.last_launch_tiles())
+        got = e.read_packed()
+    assert np.array_equal(got, oracle.bit_run(start, w, 3 * K - 1))
+
+
+def test_tile_codes_outside_the_list_rejected(gol, monkeypatch):
+    """An instantiation no parity test pins is refused at create (product build)."""
+    if os.environ.get("GOL_AMD_LIB", "").endswith("_tools.so"):
+        pytest.skip("tools build accepts them")
+    from gol import _native as N
+    for code in (5, 148, 302, 1012):
+        monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+        monkeypatch.setenv("GOL_TILE", f"14,{code}")
+        with pytest.raises(N.GolError) as ei:
+            _engine(gol, 4224, 157, band_rows=60, turns_per_launch=8)
+        assert ei.value.code == -1
 
 
 @pytest.mark.parametrize("w,h", [(5120, 5120), (2048, 2048), (512, 512), (1024, 96)])
