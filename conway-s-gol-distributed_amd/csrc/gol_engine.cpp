@@ -1882,10 +1882,11 @@ int gol_turn_counts(gol_ctx *c, int64_t first_turn, int64_t n, int64_t *out)
     });
 }
 
-int gol_read_board(gol_ctx *c, uint8_t *out)
+namespace {
+// owned rows as 0/255 bytes (the caller holds the engine: run_read)
+int read_board_bytes(gol_ctx *c, uint8_t *out)
 {
-    if (!c || !out) return GOL_EINVAL;
-    return run_read(c, [&]() -> int {
+    {
         const size_t row_bytes = (size_t)c->cfg.width;
         if (!c->raw_turn0.empty()) {
             std::memcpy(out, c->raw_turn0.data(), c->raw_turn0.size());
@@ -1906,6 +1907,23 @@ int gol_read_board(gol_ctx *c, uint8_t *out)
             if (int rc2 = sync_checked(c)) return rc2;
         }
         return GOL_OK;
+    }
+}
+}  // namespace
+
+int gol_read_board(gol_ctx *c, uint8_t *out)
+{
+    if (!c || !out) return GOL_EINVAL;
+    return run_read(c, [&]() -> int { return read_board_bytes(c, out); });
+}
+
+int gol_get_world(gol_ctx *c, uint8_t *out, int64_t *turn)
+{
+    if (!c || !out || !turn) return GOL_EINVAL;
+    return run_read(c, [&]() -> int {
+        const int rc = read_board_bytes(c, out);
+        if (rc == GOL_OK) *turn = c->turn;
+        return rc;
     });
 }
 

@@ -12,8 +12,8 @@
 //   * TurnComplete{t} is emitted for every turn when enabled (event.go:55-60
 //     contract; the reference emits none: Local/gol/distributor.go:184-185);
 //   * control keys are sampled at kernel-launch boundaries (a launch fuses up to
-//     turns_per_launch turns; multi-strip runs: chunk boundaries of a few ms) instead
-//     of after every single turn;
+//     turns_per_launch turns; multi-strip runs: chunk boundaries, ~2 chunks of ~1-4 ms
+//     each in flight) instead of after every single turn;
 //   * boards need not be square (the reference reads H x H bytes:
 //     Local/gol/distributor.go:80).
 #include <hip/hip_runtime.h>
@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -222,6 +223,11 @@ struct gol_run {
         std::lock_guard<std::mutex> lk(mu);
         closed = true;
         cv_pop.notify_all();
+    }
+    bool has_key()
+    {
+        std::lock_guard<std::mutex> lk(kmu);
+        return !keys.empty();
     }
     bool pop_key(int &k)
     {
@@ -565,6 +571,53 @@ void gol_run::run()
 
     long long chunk = 1;
     bool quit = false, killed = false;
+    // Chunks in flight: the engines' launches are enqueued without a host sync per chunk; the
+    // host waits only for the chunk before the newest one, so the GPUs never idle between
+    // chunks (a sync per chunk left a launch-latency bubble each ~4 ms) and a key or a tick is
+    // served within ~2 chunks.  Strip runs get the same bound as a single engine's control
+    // word gives it (their engines stay in lockstep: no per-engine STOP).
+    struct Chunk {
+        long long first = 0, n = 0;
+        std::vector<hipEvent_t> ev;
+    };
+    std::deque<Chunk> inflight;
+    auto drop_events = [&]() {
+        for (Chunk &c : inflight)
+            for (hipEvent_t e : c.ev) (void)hipEventDestroy(e);
+        inflight.clear();
+    };
+    struct InflightScope {
+        std::function<void()> f;
+        ~InflightScope() { f(); }
+    } inflight_scope{drop_events};
+    // wait until at most `keep` chunks are in flight; TurnComplete for the retired turns
+    auto retire = [&](size_t keep) -> bool {
+        while (inflight.size() > keep) {
+            Chunk &c = inflight.front();
+            for (size_t i = 0; i < c.ev.size(); i++) {
+                const hipError_t e = hipEventSynchronize(c.ev[i]);
+                (void)hipEventDestroy(c.ev[i]);
+                c.ev[i] = nullptr;
+                if (e != hipSuccess) {
+                    for (size_t j = i + 1; j < c.ev.size(); j++) (void)hipEventDestroy(c.ev[j]);
+                    c.ev.clear();
+                    inflight.pop_front();
+                    die(std::string("chunk wait: ") + hipGetErrorString(e));
+                    return false;
+                }
+            }
+            if (emit_turn_complete)
+                for (long long t = 1; t <= c.n; t++)
+                    if (!send(make_ev(GOL_EV_TURN_COMPLETE, c.first + t))) {
+                        c.ev.clear();
+                        inflight.pop_front();
+                        return false;
+                    }
+            c.ev.clear();
+            inflight.pop_front();
+        }
+        return true;
+    };
     struct CtlScope {   // the key thread may interrupt this run's engine while it lives
         gol_run *r;
         CtlScope(gol_run *r_, gol_ctx *e) : r(r_) { r->set_ctl_engine(e); }
@@ -575,6 +628,10 @@ void gol_run::run()
         // re-arm before draining the keys: a key pushed from here on stops the next chunk
         if (!st.strip_mode()) (void)gol_set_control(st.eng[0], GOL_CONTROL_RUN);
         int k;
+        if (has_key()) {                              // keys see every enqueued turn done
+            if (!retire(0)) return close();
+            if (st.sync()) return die(st.err);
+        }
         while (!quit && pop_key(k)) {
             if (k == 's') {                           // distributor.go:131-144
                 if (!save_image(turn)) return close();
@@ -601,16 +658,41 @@ void gol_run::run()
             }
         }
         if (quit) break;
+        if (Clock::now() >= next_tick && !retire(0)) return close();
         if (!tick()) return close();
 
         const long long want = std::min(chunk, p.turns - turn);
         const auto t0 = Clock::now();
         const long long before = st.engine_turn();
-        if (st.step(want) || st.sync()) return die(st.err);
+        if (st.step(want)) return die(st.err);
         const long long n = st.engine_turn() - before;   // < want if a key interrupted it
-        const double ms =
-            std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
-        if (emit_cell_flipped) {
+        if (!emit_cell_flipped) {
+            Chunk c;
+            c.first = turn;
+            c.n = n;
+            for (auto *e : st.eng) {
+                hipEvent_t ev = nullptr;
+                if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                    hipEventRecord(ev, (hipStream_t)gol_get_stream(e)) != hipSuccess) {
+                    if (ev) (void)hipEventDestroy(ev);
+                    for (hipEvent_t x : c.ev) (void)hipEventDestroy(x);
+                    return die("chunk event: HIP error");
+                }
+                c.ev.push_back(ev);
+            }
+            inflight.push_back(std::move(c));
+            turn += n;
+            if (!retire(1)) return close();
+            // aim for ~2 ms of GPU work per chunk: with one chunk queued behind the running
+            // one, an iteration takes about a chunk's GPU time
+            const double ms =
+                std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+            if (ms < 1.0) chunk = std::min<long long>(chunk * 2, 1 << 20);
+            else if (ms > 4.0 && chunk > 1) chunk /= 2;
+            continue;
+        }
+        if (st.sync()) return die(st.err);
+        {
             HostBuf cur;
             if (st.read_board(cur)) return die(st.err);
             // with CellFlipped on, chunks are single turns so every flip is reported
@@ -628,12 +710,9 @@ void gol_run::run()
             for (long long t = 1; t <= n; t++)
                 if (!send(make_ev(GOL_EV_TURN_COMPLETE, turn + t))) return close();
         turn += n;
-        if (!emit_cell_flipped) {
-            // aim for ~4 ms of GPU work per chunk
-            if (ms < 2.0) chunk = std::min<long long>(chunk * 2, 1 << 20);
-            else if (ms > 8.0 && chunk > 1) chunk /= 2;
-        }
     }
+    if (!retire(0)) return close();
+    if (st.sync()) return die(st.err);
 
     // retain the final board for a later CONT=yes run; 'k' kills the "server" and its state
     {

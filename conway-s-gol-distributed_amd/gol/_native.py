@@ -127,6 +127,7 @@ SIGNATURES = {
     "gol_snapshot": (_i32, [_vp, _i64p, _i64p]),
     "gol_turn_counts": (_i32, [_vp, _i64, _i64, _i64p]),
     "gol_read_board": (_i32, [_vp, _u8p]),
+    "gol_get_world": (_i32, [_vp, _u8p, _i64p]),
     "gol_read_packed": (_i32, [_vp, _u64p]),
     "gol_alive_cells": (_i32, [_vp, _i64p, _i64, _i64p]),
     "gol_export_halo": (_i32, [_vp, _vp, _vp, _vp]),

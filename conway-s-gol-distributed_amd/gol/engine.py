@@ -164,6 +164,14 @@ class Engine:
         self._c(self._L.gol_read_board(self._h, out.ctypes.data_as(N._u8p)))
         return out
 
+    def get_world(self):
+        """(board bytes, turn): the reference's GetWorld reply {SWorld, TurnCur}, one
+        consistent pair even while another thread's step() runs."""
+        out = np.zeros((self.rows, self.width), dtype=np.uint8)
+        t = ctypes.c_int64()
+        self._c(self._L.gol_get_world(self._h, out.ctypes.data_as(N._u8p), ctypes.byref(t)))
+        return out, int(t.value)
+
     def read_packed(self) -> np.ndarray:
         out = np.zeros((self.rows, self.words_per_row), dtype=np.uint64)
         self._c(self._L.gol_read_packed(self._h, out.ctypes.data_as(N._u64p)))

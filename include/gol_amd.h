@@ -30,8 +30,8 @@
  *     (Local/gol/io.go:42-143).
  *
  * Threading: one thread drives an engine (gol_step, loads, halo calls).  The read-only
- * calls (gol_snapshot, gol_get_info, gol_read_board, gol_read_packed, gol_alive_cells,
- * gol_turn_counts) may come from other threads at any time: during a gol_step the stepping
+ * calls (gol_snapshot, gol_get_info, gol_read_board, gol_get_world, gol_read_packed,
+ * gol_alive_cells, gol_turn_counts) may come from other threads at any time: during a gol_step the stepping
  * thread serves them at its next launch boundary, on a turn-consistent board; while the
  * step is parked on GOL_CONTROL_PAUSE they run at once (the reference Server's mutex is
  * held only around the per-turn commit: Server/gol/distributor.go:62-75,131-134).  A run
@@ -196,6 +196,11 @@ int gol_turn_counts(gol_ctx *ctx, int64_t first_turn, int64_t n, int64_t *out);
 /* Owned rows as bytes (rows x width, 0/255; at turn 0 the loaded bytes as-is,
  * matching the reference's Turns = 0 output). */
 int gol_read_board(gol_ctx *ctx, uint8_t *out);
+/* GetWorld (Server/gol/distributor.go:62-67, the reply ItemW{SWorld, TurnCur}): the owned
+ * rows as bytes, as gol_read_board, and the turn that board is at -- one consistent pair,
+ * callable from another thread while gol_step runs (served at a launch boundary) or is
+ * parked.  The 's' key of a controller that runs the whole game in one gol_step uses it. */
+int gol_get_world(gol_ctx *ctx, uint8_t *out, int64_t *turn);
 /* Owned rows as packed words (rows x words_per_row). */
 int gol_read_packed(gol_ctx *ctx, uint64_t *out);
 /* Row-major alive-cell list {x, y} (y = global row) of the owned rows, as

@@ -159,6 +159,54 @@ def test_multi_strip_run(gol, workdir, ngpus):
     assert (workdir / "out" / "512x512x100.pgm").read_bytes() == G.check_pgm_bytes(512, 100)
 
 
+@pytest.mark.parametrize("ngpus", (1, 4))
+def test_run_keys_mid_run_match_oracle(gol, workdir, oracle, ngpus):
+    """Keys in the middle of an unbounded run, single engine and 4 strips (the strips'
+    chunks are pipelined two deep, with no host sync per chunk): the ticker's counts, the
+    's' image at its reported turn, a pause, and 'q' all match the oracle at the turns the
+    events report (Local/gol/distributor.go:107-167)."""
+    series = G.alive_series(512)
+    p = gol.Params(Turns=100000000, Threads=8, ImageWidth=512, ImageHeight=512)
+    events, keys = gol.Channel(), gol.Channel(10)
+    kw = dict(ngpus=ngpus, devices=[0] * ngpus, halo=7) if ngpus > 1 else {}
+    h = gol.Run(p, events, keys, image_dir=str(workdir / "images"),
+                out_dir=str(workdir / "out"), ticker_ms=150, emit_turn_complete=False, **kw)
+    ticks, saved, states, final = [], [], [], []
+    for e in events:
+        if isinstance(e, gol.AliveCellsCount):
+            assert e.CellsCount == G.expected_alive(512, e.CompletedTurns, series), e
+            ticks.append(e.CompletedTurns)
+            if len(ticks) == 2:
+                keys.send("s")
+        elif isinstance(e, gol.ImageOutputComplete):
+            saved.append(e)
+            if len(saved) == 1:
+                keys.send("p")
+        elif isinstance(e, gol.StateChange):
+            states.append(e)
+            if e.NewState == gol.State.Paused:
+                time.sleep(0.4)
+                keys.send("p")
+            elif e.NewState == gol.State.Executing and len(states) > 1:
+                keys.send("q")
+        elif isinstance(e, gol.FinalTurnComplete):
+            final.append(e)
+    h.wait(10)
+    assert h.error is None, h.error
+    assert [s.NewState for s in states] == [gol.State.Executing, gol.State.Paused,
+                                           gol.State.Executing, gol.State.Quitting]
+    assert states[1].CompletedTurns == states[2].CompletedTurns >= saved[0].CompletedTurns
+    start = oracle.pack(G.input_board(512))[0]
+    t = saved[0].CompletedTurns
+    assert t >= ticks[1] > ticks[0] > 0
+    snap = G.parse_pgm((workdir / "out" / f"{saved[0].Filename}.pgm").read_bytes())
+    assert np.array_equal(snap, oracle.unpack(oracle.bit_run(start, 512, t, ncores=8), 512))
+    T = final[0].CompletedTurns
+    assert len(final[0].Alive) == G.expected_alive(512, T, series)
+    fin = G.parse_pgm((workdir / "out" / f"512x512x{T}.pgm").read_bytes())
+    assert np.array_equal(fin, oracle.unpack(oracle.bit_run(start, 512, T, ncores=8), 512))
+
+
 def test_cell_flipped(gol, workdir, oracle):
     """CellFlipped for the initial alive cells and every flip, before TurnComplete."""
     p = gol.Params(Turns=3, Threads=1, ImageWidth=16, ImageHeight=16)
@@ -266,3 +314,126 @@ def test_baseline_configs_through_run(gol, workdir, oracle, key, ngpus):
     board = G.parse_pgm(out)
     words, _, nb = oracle.pack(board)
     assert nb == 0 and hashlib.sha256(words.tobytes()).hexdigest() == d["sha256"]
+
+
+# --------------------------------------- the INTEGRATION.md cgo stub, run as a C program
+HARNESS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "conway-s-gol-distributed_amd", "build", "gol_stub_harness")
+
+
+class Stub:
+    """tests/harness/gol_stub_harness.c: the cgo stub's three goroutines (main running the
+    whole game in one gol_step, keys through the control word and gol_get_world, a ticker
+    calling gol_snapshot concurrently) as pthreads; events come back one per stdout line."""
+
+    def __init__(self, workdir, size, turns, ticker_ms, turn_complete=0):
+        import subprocess
+        import threading
+        assert os.path.exists(HARNESS), "build it: make -C conway-s-gol-distributed_amd/csrc harness"
+        (workdir / "out").mkdir(exist_ok=True)
+        self.p = subprocess.Popen(
+            [HARNESS, str(size), str(size), str(turns), str(workdir / "images"),
+             str(workdir / "out"), str(ticker_ms), str(turn_complete)],
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
+        self.lines = []
+        self.cv = threading.Condition()
+        self.t = threading.Thread(target=self._pump, daemon=True)
+        self.t.start()
+
+    def _pump(self):
+        for line in self.p.stdout:
+            with self.cv:
+                self.lines.append(line.split())
+                self.cv.notify_all()
+        with self.cv:
+            self.lines.append(["EOF"])
+            self.cv.notify_all()
+
+    def events(self, timeout=60):
+        """Yield events (lists of fields) as they arrive, until CLOSED."""
+        i, deadline = 0, time.time() + timeout
+        while True:
+            with self.cv:
+                while i >= len(self.lines):
+                    left = deadline - time.time()
+                    assert left > 0, f"harness: no event within {timeout} s: {self.lines[-5:]}"
+                    self.cv.wait(left)
+                ev = self.lines[i]
+            i += 1
+            assert ev[0] not in ("ERROR", "EOF"), self.lines
+            if ev[0] == "CLOSED":
+                return
+            yield ev
+
+    def key(self, k):
+        self.p.stdin.write(k + "\n")
+        self.p.stdin.flush()
+
+    def wait(self):
+        assert self.p.wait(30) == 0
+
+
+def test_stub_harness_event_sequence(workdir, oracle):
+    """The stub's event order for a normal run (Local/gol/distributor.go:180-226), as
+    test_event_sequence checks gol.Run's: StateChange Executing at turn 0, TurnComplete 1..T,
+    FinalTurnComplete, StateChange Quitting, ImageOutputComplete WxHxT; the final image and
+    alive count match the oracle."""
+    s = Stub(workdir, 64, 10, 2000, turn_complete=1)
+    evs = list(s.events())
+    s.wait()
+    assert evs[0] == ["StateChange", "0", "Executing"]
+    assert [int(e[1]) for e in evs if e[0] == "TurnComplete"] == list(range(1, 11))
+    tail = [e for e in evs if e[0] not in ("TurnComplete", "AliveCellsCount")]
+    assert [e[0] for e in tail] == ["StateChange", "FinalTurnComplete", "StateChange",
+                                    "ImageOutputComplete"]
+    assert tail[2] == ["StateChange", "10", "Quitting"]
+    assert tail[3] == ["ImageOutputComplete", "10", "64x64x10"]
+    want = oracle.np_run(G.input_board(64), 10)
+    assert int(tail[1][2]) == int((want == 255).sum())
+    fin = G.parse_pgm((workdir / "out" / "64x64x10.pgm").read_bytes())
+    assert np.array_equal(fin, want)
+
+
+def test_stub_harness_keys_and_ticker(workdir, oracle):
+    """The stub's keys and ticker, as test_keys_save_pause_quit and TestAlive check gol.Run's:
+    's' writes the board at the GetWorld turn, 'p' parks the single gol_step (Paused and
+    Executing report the same turn), the ticker's AliveCellsCount keeps firing while paused at
+    the paused turn, 'q' ends the run; every count and image matches the oracle."""
+    series = G.alive_series(512)
+    s = Stub(workdir, 512, 100000000, 100)
+    s.key("s")
+    saved, states, final, ticks, paused_ticks = [], [], [], [], []
+    paused_at = None
+    for e in s.events():
+        if e[0] == "ImageOutputComplete":
+            saved.append(e)
+            if len(saved) == 1:
+                s.key("p")
+        elif e[0] == "StateChange":
+            states.append(e)
+            if e[2] == "Paused" and paused_at is None:
+                paused_at = int(e[1])
+                time.sleep(0.5)
+                s.key("p")
+            elif e[2] == "Executing" and paused_at is not None:
+                s.key("q")
+        elif e[0] == "AliveCellsCount":
+            t, n = int(e[1]), int(e[2])
+            assert n == G.expected_alive(512, t, series), e
+            ticks.append(t)
+            if paused_at is not None and len(states) == 2:
+                paused_ticks.append(t)
+        elif e[0] == "FinalTurnComplete":
+            final.append(e)
+    s.wait()
+    assert [x[2] for x in states] == ["Executing", "Paused", "Executing", "Quitting"]
+    assert states[1][1] == states[2][1]
+    # (a tick whose snapshot was served just before the step parked may print after Paused)
+    assert paused_ticks.count(paused_at) >= 2 and max(paused_ticks) == paused_at
+    t = int(saved[0][1])
+    assert saved[0][2] == f"512x512x{t}"
+    snap = G.parse_pgm((workdir / "out" / f"512x512x{t}.pgm").read_bytes())
+    assert np.array_equal(snap, oracle.np_run(G.input_board(512), t))
+    T = int(final[0][1])
+    assert T >= paused_at and int(final[0][2]) == G.expected_alive(512, T, series)
+    assert saved[-1] == ["ImageOutputComplete", str(T), f"512x512x{T}"]
