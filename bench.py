@@ -102,17 +102,24 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(size, k):
+def pmc_traffic(size, k, shape=None):
     """HBM traffic per launch of the stencil from the newest committed rocprofv3 PMC pass
-    for this board size and k (profiles/rNN_k{k}_{size}_summary.json, written by
-    tools/profile.sh + tools/summarize_profile.py), or None."""
+    for this board size, depth k and -- when the summary records one -- launch shape
+    (profiles/rNN_k{k}_{size}*_summary.json, written by tools/profile.sh +
+    tools/summarize_profile.py): a summary whose `shape` differs from the launch that ran is
+    not used, so `traffic` always comes from the kernel the bench timed.  None if no pass."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_k{k}_{size}_summary.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_k{k}_{size}*_summary.json")))
     for path in reversed(files):                 # the newest pass that holds PMC bytes
         with open(path) as f:
             d = json.load(f)
-        if d.get("traffic_bytes_per_launch"):
-            return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+        if not d.get("traffic_bytes_per_launch"):
+            continue
+        if "shape" in d and shape is not None and d["shape"] != shape:
+            continue
+        if "shape" not in d and shape is not None and shape.get("kernel") == 15:
+            continue                             # (older passes: shape unknown)
+        return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -212,6 +219,7 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
     plan = eng.last_launches()          # the last gol_step call's launches (N > 1: one window)
+    tiles = eng.last_launch_tiles()     # (tile width in lanes, segment code, waves) of each
     info = eng.info()
     launches = info.launches - launches0
     exchanges = getattr(runner, "exchanges", 0) - exchanges0
@@ -226,7 +234,8 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
     out = {"W": W, "H": H, "steps": steps, "wall": wall, "gpu_ms": gpu_ms,
            "launches": launches, "K": info.turns_per_launch, "rows_local": rows_local,
            "band": info.band_rows, "fast": bool(info.fast_path), "halo": info.halo,
-           "transport": transport, "overlap": overlap, "plan": plan, "seed": seed,
+           "transport": transport, "overlap": overlap, "plan": plan, "tiles": tiles,
+           "seed": seed,
            "exchanges": exchanges, "alive": alive}
     eng.close()
     return out
@@ -248,16 +257,36 @@ def kernel_depth(plan, default):
     return text, kvar, max((k for k, v, _ in plan if v == kvar), default=default)
 
 
+def launch_shape(plan, tiles, kvar, kdepth):
+    """The shape of the dominant kernel's deepest launch: kernel, turns, band rows and, for
+    k_step_tile, the tile (width in words, height, rows per lane segment, turn order, words
+    per lane, waves per workgroup) -- what the profiles in profiles/ must have measured."""
+    for (k, v, band), t in zip(plan, tiles or [(0, 0, 0)] * len(plan)):
+        if v == kvar and k == kdepth:
+            sh = {"kernel": v, "turns": k, "band_rows": band}
+            if v == 15 and t[0] > 0:
+                tw, code, waves = t
+                words = code // 1000 + 1
+                sh["tile"] = {"code": code, "width_words": tw * words, "width_lanes": tw,
+                              "height_rows": band, "seg_rows": code % 100,
+                              "turn_order": code // 100 % 10, "words_per_lane": words,
+                              "waves_per_workgroup": waves}
+            return sh
+    return {"kernel": kvar, "turns": kdepth}
+
+
 def config_entry(c, label, world, parallel):
     """configs_measured entry: GCUPS, launch plan, roofline fractions of one measure()."""
     g = c["W"] * c["H"] * c["steps"] / c["wall"] / 1e9
     lu = c["gpu_ms"] * 1e3 / max(c["launches"], 1)
     b = BYTES_PER_CELL_UPDATE * c["rows_local"] * c["W"]
     text, kvar, kd = kernel_depth(c["plan"], c["K"])
-    traffic, src = pmc_traffic(c["W"], kd)
+    shape = launch_shape(c["plan"], c.get("tiles"), kvar, kd)
+    traffic, src = pmc_traffic(c["W"], kd, shape)
     e = {"workload": label, "value": round(g, 2), "unit": "GCUPS", "n_gpus": world,
          "ms_per_step": round(c["wall"] * 1e3 / c["steps"], 6), "parallelism": parallel,
-         "band_rows": c["band"], "temporal_blocking_k": kd,
+         "band_rows": shape.get("band_rows", c["band"]), "temporal_blocking_k": kd,
+         "launch_shape": shape,
          "kernel": KERNELS.get(kvar, f"kernel {kvar}").replace("<K>", f"<K={kd}>"),
          "launch_plan": text[:300], "traffic": traffic, "traffic_source": src,
          "launch_us": round(lu, 3), "launches": c["launches"],
@@ -410,7 +439,8 @@ def main():
         bytes_k1 = BYTES_PER_CELL_UPDATE * turns_per_launch * cells_local
         achieved = bytes_board / (launch_us * 1e-6) / 1e9
         plan_text, kvar, kdepth = kernel_depth(m["plan"], K)
-        traffic, traffic_src = pmc_traffic(W, kdepth)
+        shape = launch_shape(m["plan"], m.get("tiles"), kvar, kdepth)
+        traffic, traffic_src = pmc_traffic(W, kdepth, shape)
         out = {
             "metric": METRIC,
             "value": round(gcups, 2),
@@ -429,8 +459,9 @@ def main():
                                    f"per launch",
                        "board": [W, H], "turns": a.steps,
                        "parallelism": parallelism(a, world, m),
-                       "band_rows": m["band"], "fast_path": m["fast"],
+                       "band_rows": shape.get("band_rows", m["band"]), "fast_path": m["fast"],
                        "temporal_blocking_k": kdepth,
+                       "launch_shape": shape,
                        "launch_plan": plan_text},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -191,6 +191,7 @@ constexpr int kTileCodes[] = {
     2,    3,    4,    6,    8,    12,   16,   24,   32,   40,   48,             // ORD 0, W 1
     102,  103,  104,  106,  108,  112,  116,  124,  132,  140,                  // ORD 1
     203,  204,  206,  208,  212,  216,  224,  232,  240,                        // ORD 2
+    403,  404,  406,  408,  412,  416,  424,  432,  440,                        // ORD 4
     1002, 1003, 1004, 1006, 1008,                                               // W 2
     1102, 1103, 1104, 1106, 1108,
     1204, 1206, 1208,

@@ -42,11 +42,16 @@ namespace golk {
 
 constexpr int kTileMaxWaves = 16;                       // 1024 threads per workgroup
 // dynamic LDS of a workgroup of `threads` threads: row sums of the segments' edge rows (16 B
-// per word of the lane), first and last row, two turn parities
-constexpr size_t tile_lds_bytes(int threads, int words) { return (size_t)threads * 4 * 16 * words; }
+// per word of the lane), first and last row, two turn parities; then one progress flag per
+// wave (ORD 4), 64 B
+constexpr size_t tile_lds_bytes(int threads, int words)
+{
+    return (size_t)threads * 4 * 16 * words + 4 * kTileMaxWaves;
+}
 // tile_seg = SEG + 100 * ORD + 1000 * (W - 1): rows per lane segment, turn order (0: in order;
-// 1: interior rows, then the edge rows; 2: the same with the barrier after the interior rows),
-// words per lane
+// 1: interior rows, then the edge rows; 2: the same with the barrier after the interior rows;
+// 4: ORD 1 with no workgroup barrier -- each wave waits only for its two neighbour waves'
+// published edge sums, through per-wave progress flags in LDS), words per lane
 constexpr int tile_seg_rows(int code) { return code % 100; }
 constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 
@@ -54,6 +59,7 @@ constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 // words are neighbours, so only the outer edges need a lane shift: per row 2 DPP + 2W funnel
 // shifts + 4W v_bitop3 instead of W x (2 + 2 + 4) -- 48 instead of 52 SIMD cycles per 4096
 // cell-updates with the rule.
+// (ORD 4 up to SEG 16: held to 64 VGPRs, 8 waves per SIMD -- two 16-wave workgroups per CU)
 template <int SEG, int ORD, int W>
 __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restrict__ in,
                                                      uint64_t *__restrict__ out, StepArgs a,
@@ -198,7 +204,88 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
     // later turn or the final store needs (its rows are < K, resp. >= K + TH), and the
     // workgroup barrier no longer counts it once it has ended.
     const int wrow0 = wave * G * SEG, wrow1 = wrow0 + G * SEG;  // the wave's tile rows
-    auto turn = [&](auto P, int poff) {
+    // ORD 4: per-wave progress flags after the slot arrays.  flag[w] = the last turn whose
+    // edge sums wave w has published (-1 before the first; INT_MAX once it has left), written
+    // by lane 0 after its sums: the LDS serves one wave's requests in issue order, so a wave
+    // that reads flag[w] >= t reads w's turn-t sums (the K1w hand-off assumption).
+    // The sums are double-buffered by turn parity: a wave overwrites its turn-(t-2) slots only
+    // after both neighbours published turn t-1, i.e. after they finished reading turn t-2.
+    const int nwaves = (int)(blockDim.x >> 6);
+    volatile int *const flag = (volatile int *)(xsh + 4 * (size_t)nslot * W);
+    if constexpr (ORD == 4) {
+        if (lane == 0) flag[wave] = -1;
+        __syncthreads();                                  // (once per launch)
+    }
+    auto publish = [&](int t) {
+        if constexpr (ORD == 4) {
+            asm volatile("" ::: "memory");
+            if (lane == 0) flag[wave] = t;
+        }
+    };
+    auto await_neighbours = [&](int t) {
+        if constexpr (ORD == 4) {
+            const int up = wave > 0 ? wave - 1 : wave, dn = wave + 1 < nwaves ? wave + 1 : wave;
+            for (;;) {
+                const int a = __builtin_amdgcn_readfirstlane(flag[up]);
+                const int b = __builtin_amdgcn_readfirstlane(flag[dn]);
+                if (a >= t && b >= t) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+    };
+    // ORD 4's turn: the edge sums F (row 0) and Lr (row SEG-1) go to LDS and are read back
+    // from the wave's own slots when needed, instead of staying live across the interior rows
+    // and the wait (64 VGPRs at SEG 16: 8 waves per SIMD)
+    auto turn4 = [&](auto P, int poff, int t) {
+        constexpr int p = decltype(P)::value;
+        const int off = poff;
+        uint32_t Pw[NS], Q[NS], S1[NS];
+        {
+            uint32_t F[NS], Lr[NS];
+            rsum(v[0], F);
+            rsum(v[SEG - 1], Lr);
+            put(wtop(p, off), F);
+            put(wbot(p, off), Lr);
+            publish(t);
+#pragma unroll
+            for (int k = 0; k < NS; ++k) Pw[k] = F[k];
+        }
+        rsum(v[1], Q);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) S1[k] = Q[k];
+#pragma unroll
+        for (int i = 1; i + 1 < SEG; ++i) {
+            uint32_t R[NS];
+            if (i + 2 == SEG) get(wbot(p, off), R);   // (own bottom slot: Lr)
+            else rsum(v[i + 1], R);
+            rule(Pw, Q, R, v[i]);
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                Pw[k] = Q[k];
+                Q[k] = R[k];
+            }
+        }
+        // (keep the wait after the interior rows: the compiler would otherwise sink them
+        // below the poll loop)
+#pragma unroll
+        for (int i = 1; i + 1 < SEG; ++i)
+#pragma unroll
+            for (int d = 0; d < ND; ++d) asm volatile("" : "+v"(v[i][d]));
+        await_neighbours(t);
+        uint32_t U[NS], D[NS], F[NS];
+        get(rup(p, off), U);
+        get(wtop(p, off), F);
+        rule(U, F, S1, v[0]);
+        get(rdn(p, off), D);
+        get(wbot(p, off), F);                                 // (Lr)
+        rule(Pw, F, D, v[SEG - 1]);
+    };
+    auto turn = [&](auto P, int poff, int t) {
+        if constexpr (ORD == 4) {
+            turn4(P, poff, t);
+            return;
+        }
         constexpr int p = decltype(P)::value;
         const int off = poff;
         // the segment's first and last row sums go to the neighbours (row sums, not rows: no
@@ -284,18 +371,23 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
         }
     };
     const int lastrow = 2 * K + TH - 1;
+    auto leave = [&]() {                                 // (ORD 4: neighbours stop waiting)
+        if constexpr (ORD == 4) {
+            if (lane == 0) flag[wave] = 0x7fffffff;
+        }
+    };
     if constexpr (!kPairs) {
         for (int t = 0; t < K; ++t) {
-            if (wrow1 <= t || wrow0 > lastrow - t) return;   // (wave-uniform)
-            turn(std::integral_constant<int, 0>{}, (t & 1) * 2 * nslot);
+            if (wrow1 <= t || wrow0 > lastrow - t) return leave();   // (wave-uniform)
+            turn(std::integral_constant<int, 0>{}, (t & 1) * 2 * nslot, t);
         }
     } else {
         for (int t = 0; t < K; t += 2) {
-            if (wrow1 <= t || wrow0 > lastrow - t) return;
-            turn(std::integral_constant<int, 0>{}, 0);
+            if (wrow1 <= t || wrow0 > lastrow - t) return leave();
+            turn(std::integral_constant<int, 0>{}, 0, t);
             if (t + 1 == K) break;
-            if (wrow1 <= t + 1 || wrow0 > lastrow - t - 1) return;
-            turn(std::integral_constant<int, 1>{}, 0);
+            if (wrow1 <= t + 1 || wrow0 > lastrow - t - 1) return leave();
+            turn(std::integral_constant<int, 1>{}, 0, t + 1);
         }
     }
     // interior rows [K, K + TH) of the tile, below row_hi; interior columns inside the row

@@ -24,7 +24,7 @@ static void *tile_fn(int seg)
     case 32: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<32, ORD, 1>) : nullptr;
     case 40: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<40, ORD, 1>) : nullptr;
     case 48: return W == 1 && ORD == 0 ? reinterpret_cast<void *>(&k_step_tile<48, 0, 1>) : nullptr;
-    // (ORD 2 at SEG < 3 is ORD 1: no interior row)
+    // (ORD 2 at SEG < 3 is ORD 1: no interior row; ORD 4: SEG 3..40, one word per lane)
     default: return nullptr;
     }
 }
@@ -35,7 +35,9 @@ void *tile_kernel(int code)
 #if GOL_TOOLS   // ORD 3: no barrier between turns (wrong boards): what the turn's sync costs
     if (ord == 3 && w == 1) return tile_fn<3, 1>(seg);
 #endif
-    if (code < 0 || ord > 2 || w > 2) return nullptr;
+    if (code < 0 || w > 2) return nullptr;
+    if (ord == 4) return w == 1 && seg >= 3 && seg <= 40 ? tile_fn<4, 1>(seg) : nullptr;
+    if (ord > 2) return nullptr;
     if (w == 2) return ord == 2 ? tile_fn<2, 2>(seg) : ord ? tile_fn<1, 2>(seg) : tile_fn<0, 2>(seg);
     return ord == 2 ? tile_fn<2, 1>(seg) : ord ? tile_fn<1, 1>(seg) : tile_fn<0, 1>(seg);
 }

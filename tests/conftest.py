@@ -24,6 +24,7 @@ tools_only = pytest.mark.skipif(not TOOLS_LIB, reason="tools-build kernel (GOL_A
 TILE_CODES = (2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
               102, 103, 104, 106, 108, 112, 116, 124, 132, 140,
               203, 204, 206, 208, 212, 216, 224, 232, 240,
+              403, 404, 406, 408, 412, 416, 424, 432, 440,
               1002, 1003, 1004, 1006, 1008,
               1102, 1103, 1104, 1106, 1108,
               1204, 1206, 1208)

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define OP8(INS)                                                                             \
@@ -126,6 +127,13 @@ int main(int argc, char **argv)
     const int iters = argc > 1 ? std::atoi(argv[1]) : 20000;
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+    if (argc > 2 && std::string(argv[2]) == "occupancy") {
+        // the stencil's mix and the lone bitop3 at every resident-wave count 1..8 per SIMD
+        for (int W = 1; W <= 8; ++W) run<12>(W, iters, ncu);
+        for (int W = 1; W <= 8; ++W) run<0>(W, iters, ncu);
+        for (int W = 1; W <= 8; ++W) run<10>(W, iters, ncu);
+        return 0;
+    }
     sweep<0>(iters, ncu);
     sweep<1>(iters, ncu);
     sweep<2>(iters, ncu);

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-4 probe on one GPU box: ORD 4 (neighbour-flag) tile parity, the stencil mix's issue
+# rate at every occupancy, 65536^2 tile shapes at K = 20 (the driver's 20-turn launch) with
+# the barrier (ORD 1) and with neighbour flags (ORD 4), then SQ counter passes.
+# Each step has its own limit; a failing step ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+mkdir -p gpurun_out
+step() { local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
+  echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log"
+  [ $rc -eq 0 ] || exit $rc; }
+if [ -n "${PARITY:-1}" ]; then
+  step ord4_parity 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "tile_code_pinned and (403 or 404 or 406 or 408 or 412 or 416 or 424 or 432 or 440)"
+fi
+[ -n "${CALIB:-1}" ] && step calib_occ 120 tools/calib/valu_issue 20000 occupancy
+SHAPES=${SHAPES:-14:984:116:20,14:984:416:20,30:472:116:20,30:472:416:20,30:600:140:20,30:600:440:20,30:536:124:20,30:536:424:20,30:1240:140:20,30:1240:440:20,62:600:140:20,62:600:440:20}
+step sweep65c 400 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes "$SHAPES"
+if [ -n "${PMC:-}" ]; then
+  step pmc_s16 200 env TAG=_s16 bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 20 --band 984 --tile 14,116 --turns 100
+  step pmc_s40 200 env TAG=_s40 bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 20 --band 600 --tile 30,140 --turns 100
+fi
