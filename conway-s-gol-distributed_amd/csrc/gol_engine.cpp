@@ -52,6 +52,7 @@ constexpr size_t kStagingBytes = 256u << 20;  // byte staging chunk for load / r
 struct Launch {
     int k = 0, var = 0, band = 0;
     int tw = 0, seg = 0;
+    int blk = 0;                             // kMultiTilePersist: turns per block
 };
 constexpr int kPlanMax = 128;               // launch plans cover gol_step / halo windows up to this
 constexpr int kSeqMax = 32;                 // gol_step calls this short run a timed sequence
@@ -121,6 +122,13 @@ struct gol_ctx {
     // k_step_tile shape (kMultiTile): tile width in words, rows per lane segment (the tile
     // height is the launch's band)
     int tile_w = 0, tile_seg = 0;
+    // K1p (k_tile_persist, small torus boards): turns per block (0 = off), the uncached block
+    // buffers and per-tile flags, and the flags' epoch (grows by blocks + 1 per launch)
+    int persist_k = 0;
+    uint64_t *pu[2] = {nullptr, nullptr};
+    unsigned *pflags = nullptr;
+    size_t pflags_n = 0;
+    unsigned pepoch = 0;
     // device error word (host-mapped pinned memory; golk::kDevErr*): a k_step_wg wait that gave
     // up writes it, every synchronising call checks it
     unsigned *h_err = nullptr, *d_err = nullptr;
@@ -195,7 +203,7 @@ struct TuneKey {
     }
 };
 struct TuneVal {
-    int var, tpl, band, tile_w, tile_seg;
+    int var, tpl, band, tile_w, tile_seg, persist_k;
     float us;
     std::vector<Launch> plan;
     std::vector<std::vector<Launch>> seq;
@@ -223,8 +231,11 @@ int check_dev_err(gol_ctx *c)
     const unsigned e = c->h_err ? *(volatile unsigned *)c->h_err : 0u;
     if (!e) return GOL_OK;
     return fail(c, GOL_EHIP,
-                "a k_step_wg %s wait timed out (device error word %u): the board is corrupt; "
-                "reload it", e == golk::kDevErrPgFlag ? "parallelogram flag" : "hand-off", e);
+                "a %s wait timed out (device error word %u): the board is corrupt; reload it",
+                e == golk::kDevErrPgFlag     ? "k_step_wg parallelogram flag"
+                : e == golk::kDevErrTileFlag ? "k_tile_persist neighbour-tile flag"
+                                             : "k_step_wg hand-off",
+                e);
 }
 
 int sync_checked(gol_ctx *c)
@@ -393,6 +404,14 @@ Launch plan_launch(gol_ctx *c, int64_t room)
     if (c->tpl <= 1 || room < 2 || (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) ||
         c->blocked_pending)
         return L;
+    if (c->persist_k > 0 && !is_strip(c) && room >= 2 * c->persist_k) {
+        // K1p: blocks of <= persist_k turns in one launch, up to ~1 ms of work per launch so
+        // the control word and readers are still served every millisecond or so
+        const double us = c->tuned_us_per_turn > 0.f ? c->tuned_us_per_turn : 1.0;
+        const int64_t cap = std::max<int64_t>(2 * c->persist_k, (int64_t)(1000.0 / us));
+        return Launch{(int)std::min<int64_t>(room, cap), golk::kMultiTilePersist, c->band_multi,
+                      c->tile_w, c->tile_seg, c->persist_k};
+    }
     if (!c->plan.empty()) {
         if (room > kPlanMax)
             return Launch{c->tpl, c->multi_variant, c->band_multi, c->tile_w, c->tile_seg};
@@ -474,6 +493,40 @@ static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
     a.xlanes = (unsigned)c->pg_lanes;
     a.epoch = ++c->pg_epoch;
     return hipSuccess;
+}
+
+// K1p: the uncached block buffers (board-sized) and per-tile flags, allocated on first use
+// (the engine's streams drained first), and one launch of `turns` turns on them
+hipError_t persist_launch(gol_ctx *c, golk::StepArgs a, int turns, int K)
+{
+    const size_t words = (size_t)c->buf_rows * c->pitch;
+    const long long ntiles = golk::tile_count(c->nw, a.row_hi - a.row_lo, a.band, a.tile_w,
+                                              a.tile_seg);
+    if (!c->pu[0] || (size_t)ntiles > c->pflags_n) {
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return e;
+        for (auto *&u : c->pu)
+            if (!u && (e = hipExtMallocWithFlags((void **)&u, words * 8,
+                                                 hipDeviceMallocUncached)) != hipSuccess)
+                return e;
+        if ((size_t)ntiles > c->pflags_n) {
+            if (c->pflags) (void)hipFree(c->pflags);
+            c->pflags = nullptr;
+            c->pflags_n = 0;
+            if ((e = hipExtMallocWithFlags((void **)&c->pflags, (size_t)ntiles * sizeof(unsigned),
+                                           hipDeviceMallocUncached)) != hipSuccess ||
+                (e = hipMemset(c->pflags, 0, (size_t)ntiles * sizeof(unsigned))) != hipSuccess ||
+                (e = hipDeviceSynchronize()) != hipSuccess)
+                return e;
+            c->pflags_n = (size_t)ntiles;
+            c->pepoch = 0;
+        }
+    }
+    // flags of earlier launches are at most their epoch + blocks - 1: start above them all
+    const unsigned nblocks = (unsigned)((turns + K - 1) / K);
+    const unsigned epoch = c->pepoch + 1;
+    c->pepoch = epoch + nblocks;
+    return golk::launch_tile_persist(a, turns, K, c->pu[0], c->pu[1], c->pflags, epoch, c->stream);
 }
 
 // ---------------------------------------------------------------- k_step_tile planning
@@ -581,6 +634,7 @@ void apply_tile(gol_ctx *c, const TileShape &t)
     for (int &b : c->band_at) b = 0;
     c->plan.clear();
     c->seq.clear();
+    c->persist_k = 0;
 }
 
 // Measured search for the k_step_tile shape (coordinate descent over the launch parameters;
@@ -814,6 +868,89 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
 
 // Boards below 2^20 words (5120^2: 409 600) cannot fill the GPU with band pipelines: they run
 // k_step_tile at the measured-best shape.
+// K1p for a small torus board at the tuned tile shape: 256 turns as one k_tile_persist launch
+// (blocks of Kp turns, tiles resident between blocks) against the same turns as k_step_tile
+// launches of the tuned depth, best of 3 each; the persistent mode is kept (at its fastest
+// block depth) when it is >= 2 % faster.  Only on a device this engine has to itself: every
+// tile must be resident at once.
+void persist_tune(gol_ctx *c)
+{
+    c->persist_k = 0;
+    if (is_strip(c) || c->multi_variant != golk::kMultiTile || !device_exclusive(c->device) ||
+        getenv("GOL_NO_PERSIST"))
+        return;
+    golk::StepArgs a{};
+    a.width = c->cfg.width;
+    a.nw = c->nw;
+    a.pitch = c->pitch;
+    a.modrows = c->buf_rows;
+    a.row_lo = 0;
+    a.row_hi = c->buf_rows;
+    a.multi_words = 1;
+    a.multi_variant = golk::kMultiTile;
+    a.band = c->band_multi;
+    a.tile_w = c->tile_w;
+    a.tile_seg = c->tile_seg;
+    a.err = c->d_err;
+    const int N = 256;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return;
+    if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return; }
+    auto timed = [&](auto &&launches) -> float {       // us per turn, best of 3
+        float best = 0.f;
+        for (int pass = 0; pass < 3; ++pass) {
+            bool ok = hipEventRecord(e0, c->stream) == hipSuccess && launches() &&
+                      hipEventRecord(e1, c->stream) == hipSuccess &&
+                      hipEventSynchronize(e1) == hipSuccess;
+            float ms = 0.f;
+            if (!ok || hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return 0.f;
+            const float us = ms * 1000.f / N;
+            if (best == 0.f || us < best) best = us;
+        }
+        return best;
+    };
+    const float plain = timed([&]() {
+        const int n = (N + c->tpl - 1) / c->tpl;
+        for (int i = 0; i < n; ++i) {
+            a.in = c->board[i & 1];
+            a.out = c->board[(i + 1) & 1];
+            const int k = N / n + (i < N % n ? 1 : 0);
+            if (golk::launch_step_multi(a, k, c->stream) != hipSuccess) return false;
+        }
+        return true;
+    });
+    float best = 0.f;
+    int best_k = 0;
+    for (int Kp : {c->tpl, 8, 12, 16, 20, 24, 32}) {
+        if (Kp < 2 || !golk::tile_persist_ok(c->nw, c->buf_rows, N, Kp, c->band_multi, c->tile_w,
+                                             c->tile_seg, c->ncu))
+            continue;
+        const float us = timed([&]() {
+            a.in = c->board[0];
+            a.out = c->board[1];
+            return persist_launch(c, a, N, Kp) == hipSuccess;
+        });
+        if (getenv("GOL_AUTOTUNE_LOG"))
+            fprintf(stderr, "autotune persist %dx%d K=%d us_per_turn=%.4f (plain K=%d %.4f)\n",
+                    c->cfg.width, c->buf_rows, Kp, us, c->tpl, plain);
+        if (us > 0.f && (best == 0.f || us < best)) {
+            best = us;
+            best_k = Kp;
+        }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipGetLastError();
+    // (a wait that gave up while timing: no persistent mode, and the junk board's error word
+    // is cleared -- the board is refilled before use)
+    const bool bad = check_dev_err(c) != GOL_OK;
+    if (bad) clear_dev_err(c);
+    if (best > 0.f && plain > 0.f && best < 0.98f * plain && !bad) {
+        c->persist_k = best_k;
+        c->tuned_us_per_turn = best;
+    }
+}
+
 void autotune_small(gol_ctx *c)
 {
     float us1 = 0.f, us2 = 0.f;
@@ -823,6 +960,7 @@ void autotune_small(gol_ctx *c)
     if (!t1.K && !t2.K) return;
     apply_tile(c, two ? t2 : t1);
     c->tuned_us_per_turn = two ? us2 : us1;
+    persist_tune(c);
 }
 
 // Create-time timing sweep of the temporal-blocking kernel, its depth K and its band on
@@ -1368,6 +1506,16 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         if (c->multi_variant == golk::kMultiTile &&
             !golk::tile_shape_ok(c->nw, c->tpl, c->band_multi, c->tile_w, c->tile_seg))
             return bail(GOL_EINVAL);
+        if (const char *v = getenv("GOL_PERSIST")) {       // tests / experiments: K1p blocks
+            const int pk = atoi(v);
+            if (pk > 0) {
+                if (c->multi_variant != golk::kMultiTile || is_strip(c) ||
+                    !golk::tile_persist_ok(c->nw, c->buf_rows, 2 * pk, pk, c->band_multi,
+                                           c->tile_w, c->tile_seg, c->ncu))
+                    return bail(GOL_EINVAL);
+                c->persist_k = pk;
+            }
+        }
     }
     const char *at = getenv("GOL_AUTOTUNE");
     const bool tuning = !(cfg->flags & GOL_FLAG_NO_AUTOTUNE) && (!at || atoi(at) != 0) &&
@@ -1394,6 +1542,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
             c->band_multi = v.band;
             c->tile_w = v.tile_w;
             c->tile_seg = v.tile_seg;
+            c->persist_k = v.persist_k;
             c->plan = v.plan;
             c->seq = v.seq;
             c->tuned_us_per_turn = v.us;
@@ -1410,7 +1559,8 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         if (use_cache) {
             std::lock_guard<std::mutex> lk(g_tune_mu);
             g_tune[key] = TuneVal{c->multi_variant, c->tpl, c->band_multi, c->tile_w,
-                                  c->tile_seg, c->tuned_us_per_turn, c->plan, c->seq};
+                                  c->tile_seg, c->persist_k, c->tuned_us_per_turn, c->plan,
+                                  c->seq};
         }
     }
     if ((e = hipMemsetAsync(c->board[0], 0, words * 8, c->stream)) != hipSuccess ||
@@ -1439,6 +1589,9 @@ void gol_destroy(gol_ctx *c)
         if (c->board[1]) (void)hipFree(c->board[1]);
         if (c->pg_rows) (void)hipFree(c->pg_rows);
         if (c->pg_flags) (void)hipFree(c->pg_flags);
+        for (auto *u : c->pu)
+            if (u) (void)hipFree(u);
+        if (c->pflags) (void)hipFree(c->pflags);
         if (c->blocked) (void)hipFree(c->blocked);
         if (c->counts) (void)hipFree(c->counts);
         if (c->staging) (void)hipFree(c->staging);
@@ -1776,7 +1929,7 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
             a.counts = nullptr;
             a.band = plan.band;
             a.multi_variant = plan.var;
-            if (plan.var == golk::kMultiTile) {
+            if (plan.var == golk::kMultiTile || plan.var == golk::kMultiTilePersist) {
                 a.tile_w = plan.tw;
                 a.tile_seg = plan.seg;
             }
@@ -1785,7 +1938,9 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
                 if (int rc = wg_diag_launch(c, a, k)) return rc;
             } else
 #endif
-            if (split && in_lo < in_hi) {
+            if (plan.var == golk::kMultiTilePersist) {
+                HIP_OR_FAIL(c, persist_launch(c, a, k, plan.blk));
+            } else if (split && in_lo < in_hi) {
                 golk::StepArgs b = a;
                 // concurrent launches cannot share the published-row scratch
                 if (b.multi_variant == golk::kMultiWgPg) b.multi_variant = golk::kMultiWgHx;
@@ -1925,6 +2080,14 @@ int gol_tile_codes(int32_t *codes, int32_t cap)
     const int n = (int)std::size(golk::kTileCodes);
     if (cap < 0 || (cap > 0 && !codes)) return GOL_EINVAL;
     for (int i = 0; i < std::min(n, (int)cap); ++i) codes[i] = golk::kTileCodes[i];
+    return n;
+}
+
+int gol_tile_persist_codes(int32_t *codes, int32_t cap)
+{
+    const int n = (int)std::size(golk::kTilePersistCodes);
+    if (cap < 0 || (cap > 0 && !codes)) return GOL_EINVAL;
+    for (int i = 0; i < std::min(n, (int)cap); ++i) codes[i] = golk::kTilePersistCodes[i];
     return n;
 }
 

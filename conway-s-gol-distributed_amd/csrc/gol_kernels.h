@@ -47,6 +47,7 @@ struct StepArgs {
 // device error codes (StepArgs::err)
 constexpr unsigned kDevErrHandoff = 1u;    // k_step_wg: LDS hand-off wait timed out
 constexpr unsigned kDevErrPgFlag = 2u;     // k_step_wg parallelogram: flag wait timed out
+constexpr unsigned kDevErrTileFlag = 3u;   // k_tile_persist: a neighbour tile's flag wait timed out
 
 // temporal-blocking kernels (A/B-able via GOL_MULTI_VARIANT; kMultiSkewILW16 is shipped)
 enum : int {
@@ -74,6 +75,8 @@ enum : int {
     kMultiTile = 15,        // k_step_tile: a 2-D tile per workgroup, resident in registers for
                             //   all K turns (small boards: gol_tile.h)
     kMultiCount = 16,
+    kMultiTilePersist = 16, // K1p k_tile_persist: k_step_tile's tiles resident across blocks of
+                            //   K turns (engine-internal: small torus boards, never requested)
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 
@@ -196,6 +199,10 @@ constexpr int kTileCodes[] = {
     1102, 1103, 1104, 1106, 1108,
     1204, 1206, 1208,
 };
+// the codes k_tile_persist (K1p) is instantiated for (gol_tile.hip persist_fn; each pinned by
+// tests/test_gpu_engine.py::test_tile_persist_pinned through gol_tile_persist_codes)
+constexpr int kTilePersistCodes[] = {102, 103, 104, 106, 108, 112, 116,
+                                     403, 404, 406, 408, 412, 416};
 constexpr bool tile_code_shipped(int code)
 {
     for (int c : kTileCodes)
@@ -208,6 +215,13 @@ int tile_waves(int turns, int tile_h, int tile_w, int seg);
 int tile_blocks_per_cu(int turns, int tile_h, int tile_w, int seg);
 long long tile_count(int nw, int rows, int tile_h, int tile_w, int seg);
 hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s);
+// K1p k_tile_persist (gol_tile.h): `turns` turns in blocks of K on tiles resident for the whole
+// launch, exchanging borders between blocks through u0 / u1 (uncached, board-sized) and
+// per-tile flags (uncached, one per tile; epoch above every earlier launch's flags).
+// tile_persist_ok: an instantiated code, K within the tile rows, every tile resident at once.
+bool tile_persist_ok(int nw, int rows, int turns, int K, int tile_h, int tile_w, int seg, int ncu);
+hipError_t launch_tile_persist(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
+                               unsigned *flags, unsigned epoch, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);
 

@@ -59,11 +59,14 @@ constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 // words are neighbours, so only the outer edges need a lane shift: per row 2 DPP + 2W funnel
 // shifts + 4W v_bitop3 instead of W x (2 + 2 + 4) -- 48 instead of 52 SIMD cycles per 4096
 // cell-updates with the rule.
-// (ORD 4 up to SEG 16: held to 64 VGPRs, 8 waves per SIMD -- two 16-wave workgroups per CU)
-template <int SEG, int ORD, int W>
-__global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restrict__ in,
-                                                     uint64_t *__restrict__ out, StepArgs a,
-                                                     int turns, int ntx, int ntiles)
+// One pass of K turns over one tile (the body of k_step_tile, and of each block of
+// k_tile_persist).  PERSIST: the workgroup stays for further passes, so a wave that leaves the
+// trapezoid does not end -- it skips its remaining turns (ORD 1/2: it still meets every
+// workgroup barrier of them) and the pass returns to the caller on every path.
+template <int SEG, int ORD, int W, bool PERSIST>
+__device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
+                                          uint64_t *__restrict__ out, const StepArgs &a,
+                                          int turns, int tile, int ntx)
 {
     constexpr int ND = 2 * W;                            // dwords per lane and row
     constexpr int NS = 2 * ND;                           // row-sum dwords (2 bits per dword)
@@ -75,11 +78,6 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
     const int TW = a.tile_w, C = TW + 2, G = 64 / C;     // (in lanes of W words)
     const int K = turns, TH = a.band;
     const int nl = a.nw / W;                             // lane columns per row
-    // XCD-aware tile order: blockIdx b runs on XCD b % 8, which gets a contiguous run of
-    // tiles (whole tile rows, so most halo rows were written by the same XCD's L2)
-    const int per = (ntiles + 7) / 8;
-    const int tile = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
-    if (tile >= ntiles) return;                          // the whole workgroup
     const int ty = tile / ntx, tx = tile - ty * ntx;
     const int y0 = a.row_lo + ty * TH;
     const int x0 = tx * TW;
@@ -371,27 +369,47 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
         }
     };
     const int lastrow = 2 * K + TH - 1;
-    auto leave = [&]() {                                 // (ORD 4: neighbours stop waiting)
+    // a wave leaving the trapezoid at turn t: its rows are all < K or >= K + TH, so it has
+    // nothing to store.  Alone it ends (the barrier stops counting it); in a persistent pass
+    // it meets the K - t barriers its turns would have met (ORD 4: none -- its flag says it
+    // has gone) and falls through to the (empty) store
+    auto leave = [&](int t) {
         if constexpr (ORD == 4) {
             if (lane == 0) flag[wave] = 0x7fffffff;
+        } else if constexpr (PERSIST && ORD != 3) {
+            for (; t < K; ++t) __syncthreads();
         }
     };
+    bool gone = false;
     if constexpr (!kPairs) {
         for (int t = 0; t < K; ++t) {
-            if (wrow1 <= t || wrow0 > lastrow - t) return leave();   // (wave-uniform)
+            if (wrow1 <= t || wrow0 > lastrow - t) {           // (wave-uniform)
+                leave(t);
+                gone = true;
+                break;
+            }
             turn(std::integral_constant<int, 0>{}, (t & 1) * 2 * nslot, t);
         }
     } else {
         for (int t = 0; t < K; t += 2) {
-            if (wrow1 <= t || wrow0 > lastrow - t) return leave();
+            if (wrow1 <= t || wrow0 > lastrow - t) {
+                leave(t);
+                gone = true;
+                break;
+            }
             turn(std::integral_constant<int, 0>{}, 0, t);
             if (t + 1 == K) break;
-            if (wrow1 <= t + 1 || wrow0 > lastrow - t - 1) return leave();
+            if (wrow1 <= t + 1 || wrow0 > lastrow - t - 1) {
+                leave(t + 1);
+                gone = true;
+                break;
+            }
             turn(std::integral_constant<int, 1>{}, 0, t + 1);
         }
     }
+    if (!PERSIST && gone) return;
     // interior rows [K, K + TH) of the tile, below row_hi; interior columns inside the row
-    if (!live || col < 1 || col > TW || x0 + col - 1 >= nl) return;
+    if (gone || !live || col < 1 || col > TW || x0 + col - 1 >= nl) return;
     const int t0 = seg * SEG;
     // per-lane byte offset (the segment differs between the lane groups of a wave); rows
     // y0 - K + t0 + i are stored only once inside [row_lo, row_hi): no wrap, and the
@@ -403,6 +421,86 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
         if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) buf_store(v[i], rout, so, 0);
         so += pitch_b;
     }
+}
+
+// XCD-aware tile order: blockIdx b runs on XCD b % 8, which gets a contiguous run of tiles
+// (whole tile rows, so most halo rows were written by the same XCD's L2)
+__device__ __forceinline__ int tile_of_block(int ntiles)
+{
+    const int per = (ntiles + 7) / 8;
+    return (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+}
+
+// (ORD 4 up to SEG 16: 64 VGPRs, 8 waves per SIMD -- two 16-wave workgroups per CU)
+template <int SEG, int ORD, int W>
+__global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restrict__ in,
+                                                     uint64_t *__restrict__ out, StepArgs a,
+                                                     int turns, int ntx, int ntiles)
+{
+    const int tile = tile_of_block(ntiles);
+    if (tile >= ntiles) return;                          // the whole workgroup
+    tile_pass<SEG, ORD, W, false>(in, out, a, turns, tile, ntx);
+}
+
+// K1p k_tile_persist: `turns` turns in blocks of K on tiles that stay resident for the whole
+// launch (small boards: every tile is one resident workgroup, checked by the host).  A block
+// is one tile_pass; between blocks a tile exchanges its borders with its 8 neighbours through
+// memory instead of ending the launch: block b reads buffer u[(b-1) % 2] (block 0: `in`) and
+// writes u[b % 2] (the last block: `out`); u0 / u1 are uncached (visible across the XCDs' L2s
+// without cache maintenance, like the k_step_wg parallelogram rows).  flags[tile] = epoch + b
+// + 1 once the tile's block-b stores completed; a tile starts block b when its 8 neighbours
+// are there -- which also means they finished reading the buffer it is about to overwrite.
+// A wait that gives up after kTileSpinLimit polls marks the error word (GOL_EHIP at the next
+// synchronising call) and goes on with a wrong board rather than hang.
+#ifndef GOL_TILE_SPIN_LIMIT
+#define GOL_TILE_SPIN_LIMIT (1 << 22)
+#endif
+template <int SEG, int ORD, int W>
+__global__ __launch_bounds__(1024, 1) void k_tile_persist(
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t *u0, uint64_t *u1,
+    StepArgs a, int turns, int K, int ntx, int ntiles, unsigned *flags, unsigned epoch)
+{
+    const int tile = tile_of_block(ntiles);
+    if (tile >= ntiles) return;                          // (never waited for)
+    const int nty = ntiles / ntx, ty = tile / ntx, tx = tile - ty * ntx;
+    // ceil(turns / K) blocks of near-equal depth (<= K): 1000 turns at K = 32 run as
+    // 8 x 32 + 24 x 31, not 31 x 32 + 8
+    const int nblocks = (turns + K - 1) / K, base = turns / nblocks, extra = turns % nblocks;
+    bool gave_up = false;
+    for (int b = 0; b < nblocks; ++b) {
+        const int k = base + (b < extra ? 1 : 0);
+        if (b > 0) {
+            if (threadIdx.x < 8) {                        // one neighbour per lane 0..7
+                const int j = (int)threadIdx.x + (threadIdx.x >= 4 ? 1 : 0);   // skip (0, 0)
+                const int dy = j / 3 - 1, dx = j % 3 - 1;
+                const int ny = (ty + dy + nty) % nty, nx = (tx + dx + ntx) % ntx;
+                const unsigned want = epoch + (unsigned)b;
+                unsigned *f = flags + ny * ntx + nx;
+                bool seen = false;
+                for (int spin = 0; !seen && spin < GOL_TILE_SPIN_LIMIT; ++spin) {
+                    const unsigned v =
+                        __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    seen = (int)(v - want) >= 0;
+                    if (!seen) __builtin_amdgcn_s_sleep(2);
+                }
+                gave_up |= !seen;
+            }
+            // (the loads of the block stay below the waits: the barrier and the fence)
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __syncthreads();
+        }
+        const uint64_t *src = b == 0 ? in : ((b & 1) ? u0 : u1);
+        uint64_t *dst = b + 1 == nblocks ? out : ((b & 1) ? u1 : u0);
+        tile_pass<SEG, ORD, W, true>(src, dst, a, k, tile, ntx);
+        if (b + 1 == nblocks) break;
+        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // this wave's stores are done
+        __syncthreads();                                     // ... and every wave's
+        if (threadIdx.x == 0)
+            __hip_atomic_store(flags + tile, epoch + (unsigned)b + 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (gave_up && a.err)
+        __hip_atomic_store(a.err, kDevErrTileFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace golk

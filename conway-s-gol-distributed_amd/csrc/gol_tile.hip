@@ -1,6 +1,7 @@
 // gol_tile.hip -- the k_step_tile instantiation table (K1t, gol_tile.h) and its launcher.
 #include "gol_tile.h"
 
+#include <iterator>
 #include <map>
 #include <mutex>
 
@@ -25,6 +26,29 @@ static void *tile_fn(int seg)
     case 40: return W == 1 ? reinterpret_cast<void *>(&k_step_tile<40, ORD, 1>) : nullptr;
     case 48: return W == 1 && ORD == 0 ? reinterpret_cast<void *>(&k_step_tile<48, 0, 1>) : nullptr;
     // (ORD 2 at SEG < 3 is ORD 1: no interior row; ORD 4: SEG 3..40, one word per lane)
+    default: return nullptr;
+    }
+}
+
+// k_tile_persist instantiations (K1p, small boards): one word per lane, interior rows first
+// with the workgroup barrier (ORD 1) or with neighbour flags (ORD 4), SEG 2..16
+static void *persist_fn(int code)
+{
+    static_assert(std::size(kTilePersistCodes) == 13, "persist_fn covers kTilePersistCodes");
+    switch (code) {
+    case 102: return reinterpret_cast<void *>(&k_tile_persist<2, 1, 1>);
+    case 103: return reinterpret_cast<void *>(&k_tile_persist<3, 1, 1>);
+    case 104: return reinterpret_cast<void *>(&k_tile_persist<4, 1, 1>);
+    case 106: return reinterpret_cast<void *>(&k_tile_persist<6, 1, 1>);
+    case 108: return reinterpret_cast<void *>(&k_tile_persist<8, 1, 1>);
+    case 112: return reinterpret_cast<void *>(&k_tile_persist<12, 1, 1>);
+    case 116: return reinterpret_cast<void *>(&k_tile_persist<16, 1, 1>);
+    case 403: return reinterpret_cast<void *>(&k_tile_persist<3, 4, 1>);
+    case 404: return reinterpret_cast<void *>(&k_tile_persist<4, 4, 1>);
+    case 406: return reinterpret_cast<void *>(&k_tile_persist<6, 4, 1>);
+    case 408: return reinterpret_cast<void *>(&k_tile_persist<8, 4, 1>);
+    case 412: return reinterpret_cast<void *>(&k_tile_persist<12, 4, 1>);
+    case 416: return reinterpret_cast<void *>(&k_tile_persist<16, 4, 1>);
     default: return nullptr;
     }
 }
@@ -106,6 +130,48 @@ hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s)
     void *params[] = {&in, &out, &args, &k, &ntx_arg, &nt};
     return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params,
                            tile_lds_bytes(threads, tile_seg_words(a.tile_seg)), s);
+}
+
+}  // namespace golk
+
+namespace golk {
+
+bool tile_persist_ok(int nw, int rows, int turns, int K, int tile_h, int tile_w, int seg, int ncu)
+{
+    if (!persist_fn(seg) || !tile_shape_ok(nw, K, tile_h, tile_w, seg) || turns < 1 || ncu < 1)
+        return false;
+    const int nty = (rows + tile_h - 1) / tile_h;
+    const int last_h = rows - (nty - 1) * tile_h;
+    // a tile's K halo rows come from the adjacent tile rows only
+    if (K > tile_h || K > last_h) return false;
+    const long long ntiles = tile_count(nw, rows, tile_h, tile_w, seg);
+    const long long blocks = (ntiles + 7) / 8 * 8;
+    const int waves = tile_waves(K, tile_h, tile_w, seg);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, persist_fn(seg), 64 * waves, tile_lds_bytes(64 * waves, 1)) != hipSuccess)
+        return false;
+    // every tile resident at once: a tile waits for its neighbours
+    return per_cu > 0 && blocks <= (long long)ncu * per_cu;
+}
+
+hipError_t launch_tile_persist(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
+                               unsigned *flags, unsigned epoch, hipStream_t s)
+{
+    const int rows = a.row_hi - a.row_lo;
+    void *fn = persist_fn(a.tile_seg);
+    if (!fn || !tile_shape_ok(a.nw, K, a.band, a.tile_w, a.tile_seg) || K > rows) return hipErrorInvalidValue;
+    const int ntx = (a.nw + a.tile_w - 1) / a.tile_w;
+    const long long ntiles = (long long)ntx * ((rows + a.band - 1) / a.band);
+    if (ntiles <= 0 || ntiles > (1 << 20)) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((ntiles + 7) / 8 * 8);
+    const int threads = 64 * tile_waves(K, a.band, a.tile_w, a.tile_seg);
+    StepArgs args = a;
+    const uint64_t *in = a.in;
+    uint64_t *out = a.out;
+    int t = turns, k = K, ntx_arg = ntx, nt = (int)ntiles;
+    void *params[] = {&in, &out, &u0, &u1, &args, &t, &k, &ntx_arg, &nt, &flags, &epoch};
+    return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params, tile_lds_bytes(threads, 1), s);
 }
 
 }  // namespace golk

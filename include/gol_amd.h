@@ -169,6 +169,9 @@ int gol_last_launch_tiles(gol_ctx *ctx, int32_t *tile_w, int32_t *tile_seg, int3
  * tests: every code the shape search can pick has an oracle test).  Writes min(n, cap) codes,
  * returns n.  Needs no device. */
 int gol_tile_codes(int32_t *codes, int32_t cap);
+/* The subset of those the persistent tile kernel (K1p: small torus boards, tiles resident
+ * across blocks of turns) runs; same convention. */
+int gol_tile_persist_codes(int32_t *codes, int32_t cap);
 /* Lock-free progress read for a controlling thread: *turn = turns enqueued so far (the
  * board reaches it at the next gol_sync), *parked = 1 while gol_step is parked on PAUSE
  * (the board is then complete at *turn).  Either pointer may be NULL. */

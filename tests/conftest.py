@@ -30,6 +30,10 @@ TILE_CODES = (2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
               1204, 1206, 1208)
 
 
+# the subset the persistent tile kernel (K1p) runs (gol_tile_persist_codes)
+TILE_PERSIST_CODES = (102, 103, 104, 106, 108, 112, 116, 403, 404, 406, 408, 412, 416)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
 

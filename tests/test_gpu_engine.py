@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import golden_data as G
-from conftest import tools_only
+from conftest import TILE_CODES, TILE_PERSIST_CODES, tools_only
 
 pytestmark = pytest.mark.gpu
 
@@ -253,6 +253,13 @@ def test_launch_planner(gol, oracle):
             if turns >= 2:
                 assert all(k >= 2 for k, _, _ in plan), plan
             assert all(b > 0 for _, _, b in plan)
+            # each k_step_tile launch runs the shape it was timed at (a planner family may
+            # be another tile shape than the engine's own pick): a pinned code, <= 16 waves
+            for (k, v, b), (tw, code, waves) in zip(plan, e.last_launch_tiles()):
+                if v == 15:
+                    assert code in TILE_CODES and tw > 0 and 1 <= waves <= 16, (k, b, tw, code)
+                else:
+                    assert (tw, code, waves) == (0, 0, 0)
         got = e.read_packed()
     assert np.array_equal(got, oracle.bit_run(board, w, 68))
 
@@ -697,7 +704,7 @@ def _pinned_shape(code):
     return (14, 100) if seg <= 8 else (30, 100)   # 66 words = 4 x 14 + 10 = 2 x 30 + 6
 
 
-@pytest.mark.parametrize("code", __import__("conftest").TILE_CODES)
+@pytest.mark.parametrize("code", TILE_CODES)
 def test_tile_code_pinned(gol, oracle, monkeypatch, code):
     """Every k_step_tile instantiation the product library can run (gol_tile_codes; the shape
     searches pick only these) against the oracle: ragged tiles in both directions, one launch
@@ -719,6 +726,43 @@ def test_tile_code_pinned(gol, oracle, monkeypatch, code):
         assert all(v > 1 for _, _, v in e.last_launch_tiles())
         got = e.read_packed()
     assert np.array_equal(got, oracle.bit_run(start, w, 3 * K - 1))
+
+
+PERSIST_SHAPES = [
+    # (width, height, tile_w, tile_h, K, turns): ragged both ways, several blocks and a short
+    # last one, a single tile row / column (a tile is its own neighbour), K == last tile row
+    (4224, 157, 14, 100, 8, 43),
+    (4224, 157, 30, 60, 12, 40),
+    (1024, 64, 14, 64, 8, 35),        # one tile row: the up and down neighbours are itself
+    (896, 90, 14, 30, 10, 31),        # one tile column (14 words), 3 tile rows
+]
+
+
+@pytest.mark.parametrize("code", TILE_PERSIST_CODES)
+@pytest.mark.parametrize("shape", range(len(PERSIST_SHAPES)))
+def test_tile_persist_pinned(gol, oracle, monkeypatch, code, shape):
+    """K1p k_tile_persist (tiles resident across blocks of K turns, borders exchanged through
+    uncached memory and per-tile flags) for every instantiation it has, against the oracle:
+    one launch runs all the turns (blocks of near-equal depth), then a second call continues
+    from the first's board."""
+    w, h, tw, th, K, turns = PERSIST_SHAPES[shape]
+    if code % 100 * (64 // (tw + 2)) * 16 < th + 2 * K:
+        pytest.skip("tile taller than 16 waves of this segment")
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+    monkeypatch.setenv("GOL_TILE", f"{tw},{code}")
+    monkeypatch.setenv("GOL_PERSIST", str(K))
+    start = oracle.gen_random(code * 3 + shape, w, h)
+    with _engine(gol, w, h, band_rows=th, turns_per_launch=K) as e:
+        e.load_packed(start)
+        e.step(turns)
+        plan = e.last_launches()
+        assert [v for _, v, _ in plan] == [16] and plan[0][0] == turns, plan
+        mid = e.read_packed()
+        e.step(turns + 3)
+        got = e.read_packed()
+    want = oracle.bit_run(start, w, turns)
+    assert np.array_equal(mid, want)
+    assert np.array_equal(got, oracle.bit_run(want, w, turns + 3))
 
 
 def test_tile_codes_outside_the_list_rejected(gol, monkeypatch):
@@ -743,7 +787,8 @@ def test_small_board_default_is_tile(gol, oracle, w, h):
         e.load_packed(start)
         e.step(45)
         plan = e.last_launches()
-        assert plan and all(v == 15 and k >= 2 for k, v, _ in plan), plan
+        # (16: the same tiles resident across blocks, K1p, when the autotune measured it faster)
+        assert plan and all(v in (15, 16) and k >= 2 for k, v, _ in plan), plan
         got = e.read_packed()
     assert np.array_equal(got, oracle.bit_run(start, w, 45))
 
@@ -802,6 +847,18 @@ else:
     out = r.stdout
     assert "EHIP" in out and "timed out" in out, out
     assert "STICKY -2" in out and "CLEARED" in out, out
+    # the same for k_tile_persist's neighbour-tile flag waits
+    code_p = code.replace("gol.Engine(2048, 512, device=0, band_rows=43, turns_per_launch=16)",
+                          "gol.Engine(4224, 157, device=0, band_rows=100, turns_per_launch=8)")
+    code_p = code_p.replace("gol_step(e.handle, 16)", "gol_step(e.handle, 40)")
+    env = dict(os.environ, GOL_AMD_LIB=lib, GOL_MULTI_VARIANT="15", GOL_TILE="14,103",
+               GOL_PERSIST="8")
+    r = subprocess.run([sys.executable, "-c", code_p,
+                        os.path.join(root, "conway-s-gol-distributed_amd")],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "EHIP" in r.stdout and "neighbour-tile" in r.stdout, r.stdout
+    assert "STICKY -2" in r.stdout and "CLEARED" in r.stdout, r.stdout
 
 
 # ------------------------------------------------ concurrent reads while stepping

@@ -11,7 +11,9 @@ step() { local name=$1 t=$2; shift 2
   echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log"
   [ $rc -eq 0 ] || exit $rc; }
 if [ -n "${PARITY:-1}" ]; then
-  step ord4_parity 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "tile_code_pinned and (403 or 404 or 406 or 408 or 412 or 416 or 424 or 432 or 440)"
+  step new_tests 600 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_run.py -x -v --timeout 150 --timeout-method thread -k "tile_code or tile_persist or spin_timeout or driver_command or stub_harness or keys_mid_run or small_board or planner or event_sequence or keys_save or multi_strip or 5120"
+  step c2_auto 200 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --rounds 3
+  step c2_nopersist 200 env GOL_NO_PERSIST=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --rounds 3
 fi
 [ -n "${CALIB:-1}" ] && step calib_occ 120 tools/calib/valu_issue 20000 occupancy
 SHAPES=${SHAPES:-14:984:116:20,14:984:416:20,30:472:116:20,30:472:416:20,30:600:140:20,30:600:440:20,30:536:124:20,30:536:424:20,30:1240:140:20,30:1240:440:20,62:600:140:20,62:600:440:20}
