@@ -125,6 +125,7 @@ struct gol_ctx {
     // K1p (k_tile_persist, small torus boards): turns per block (0 = off), the uncached block
     // buffers and per-tile flags, and the flags' epoch (grows by blocks + 1 per launch)
     int persist_k = 0;
+    bool persist_forced = false;             // GOL_PERSIST (tests): also on a shared device
     uint64_t *pu[2] = {nullptr, nullptr};
     unsigned *pflags = nullptr;
     size_t pflags_n = 0;
@@ -404,7 +405,10 @@ Launch plan_launch(gol_ctx *c, int64_t room)
     if (c->tpl <= 1 || room < 2 || (c->cfg.flags & GOL_FLAG_COUNT_EVERY_TURN) ||
         c->blocked_pending)
         return L;
-    if (c->persist_k > 0 && !is_strip(c) && room >= 2 * c->persist_k) {
+    // (another engine on the device could hold CUs the resident tiles need: then plain
+    // launches -- a starved wait would give up and report GOL_EHIP, but never hang)
+    if (c->persist_k > 0 && !is_strip(c) && room >= 2 * c->persist_k &&
+        (c->persist_forced || device_exclusive(c->device))) {
         // K1p: blocks of <= persist_k turns in one launch, up to ~1 ms of work per launch so
         // the control word and readers are still served every millisecond or so
         const double us = c->tuned_us_per_turn > 0.f ? c->tuned_us_per_turn : 1.0;
@@ -1514,6 +1518,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
                                            c->tile_w, c->tile_seg, c->ncu))
                     return bail(GOL_EINVAL);
                 c->persist_k = pk;
+                c->persist_forced = true;
             }
         }
     }
