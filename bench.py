@@ -219,7 +219,8 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
     plan = eng.last_launches()          # the last gol_step call's launches (N > 1: one window)
-    tiles = eng.last_launch_tiles()     # (tile width in lanes, segment code, waves) of each
+    tiles = eng.last_launch_tiles(blocks=True)   # (tile width in lanes, segment code, waves,
+                                                 # turns per block) of each
     info = eng.info()
     launches = info.launches - launches0
     exchanges = getattr(runner, "exchanges", 0) - exchanges0
@@ -241,7 +242,8 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
     return out
 
 
-KERNELS = {7: "k_step_skew<K> (interleaved layout, one pipeline per wave)",
+KERNELS = {16: "k_tile_persist<K> (k_step_tile's 2-D tiles resident across blocks of turns)",
+           7: "k_step_skew<K> (interleaved layout, one pipeline per wave)",
            8: "k_step_wg<K> (pipeline split over a workgroup, band tiles)",
            9: "k_step_wg<K> (pipeline split over a workgroup, helix tiles)",
            12: "k_step_wg<K> (helix tiles, parallelogram bands)",
@@ -261,11 +263,13 @@ def launch_shape(plan, tiles, kvar, kdepth):
     """The shape of the dominant kernel's deepest launch: kernel, turns, band rows and, for
     k_step_tile, the tile (width in words, height, rows per lane segment, turn order, words
     per lane, waves per workgroup) -- what the profiles in profiles/ must have measured."""
-    for (k, v, band), t in zip(plan, tiles or [(0, 0, 0)] * len(plan)):
+    for (k, v, band), t in zip(plan, tiles or [(0, 0, 0, 0)] * len(plan)):
         if v == kvar and k == kdepth:
             sh = {"kernel": v, "turns": k, "band_rows": band}
-            if v == 15 and t[0] > 0:
-                tw, code, waves = t
+            if v in (15, 16) and t[0] > 0:
+                tw, code, waves, blk = t
+                if v == 16:
+                    sh["block_turns"] = blk
                 words = code // 1000 + 1
                 sh["tile"] = {"code": code, "width_words": tw * words, "width_lanes": tw,
                               "height_rows": band, "seg_rows": code % 100,

@@ -2065,17 +2065,21 @@ int gol_last_launches(gol_ctx *c, int32_t *turns, int32_t *kernel, int32_t *band
 }
 
 int gol_last_launch_tiles(gol_ctx *c, int32_t *tile_w, int32_t *tile_seg, int32_t *waves,
-                          int32_t cap)
+                          int32_t *block_turns, int32_t cap)
 {
-    if (!c || cap < 0 || (cap > 0 && (!tile_w || !tile_seg || !waves))) return GOL_EINVAL;
+    if (!c || cap < 0 || (cap > 0 && (!tile_w || !tile_seg || !waves || !block_turns)))
+        return GOL_EINVAL;
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     const int n = (int)std::min<size_t>((size_t)cap, c->last.size());
     for (int i = 0; i < n; ++i) {
         const Launch &L = c->last[i];
-        const bool t = L.k > 1 && L.var == golk::kMultiTile;
+        const bool p = L.var == golk::kMultiTilePersist;
+        const bool t = L.k > 1 && (L.var == golk::kMultiTile || p);
+        const int depth = p ? L.blk : L.k;               // (K1p: the waves fit one block)
         tile_w[i] = t ? L.tw : 0;
         tile_seg[i] = t ? L.seg : 0;
-        waves[i] = t ? golk::tile_waves(L.k, L.band, L.tw, L.seg) : 0;
+        waves[i] = t ? golk::tile_waves(depth, L.band, L.tw, L.seg) : 0;
+        block_turns[i] = t ? depth : 0;
     }
     return (int)std::min<long long>(c->last_n, 0x7fffffff);
 }

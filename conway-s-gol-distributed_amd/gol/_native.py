@@ -120,6 +120,7 @@ SIGNATURES = {
                                  ctypes.c_int32]),
     "gol_last_launch_tiles": (_i32, [_vp, ctypes.POINTER(ctypes.c_int32),
                                      ctypes.POINTER(ctypes.c_int32),
+                                     ctypes.POINTER(ctypes.c_int32),
                                      ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     "gol_tile_codes": (_i32, [ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     "gol_tile_persist_codes": (_i32, [ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),

@@ -129,12 +129,14 @@ class Engine:
         n = self._c(self._L.gol_last_launches(self._h, *arrs, int(cap)))
         return [(arrs[0][i], arrs[1][i], arrs[2][i]) for i in range(min(n, cap))]
 
-    def last_launch_tiles(self, cap: int = 4096):
-        """[(tile width, segment code, waves per workgroup)] of the same launches (k_step_tile;
-        zeros for the other kernels)."""
-        arrs = [(ctypes.c_int32 * cap)() for _ in range(3)]
+    def last_launch_tiles(self, cap: int = 4096, blocks: bool = False):
+        """[(tile width, segment code, waves per workgroup)] of the same launches (k_step_tile
+        and its persistent form; zeros for the other kernels); blocks=True adds the turns per
+        block as a fourth element."""
+        arrs = [(ctypes.c_int32 * cap)() for _ in range(4)]
         n = self._c(self._L.gol_last_launch_tiles(self._h, *arrs, int(cap)))
-        return [(arrs[0][i], arrs[1][i], arrs[2][i]) for i in range(min(n, cap))]
+        k = 4 if blocks else 3
+        return [tuple(arrs[j][i] for j in range(k)) for i in range(min(n, cap))]
 
     # -- overlapped halo exchange (gol_stream_wait / gol_step_overlap)
     def stream_wait(self, stream_ptr: int):

@@ -160,11 +160,13 @@ int gol_set_control(gol_ctx *ctx, int32_t word);
  * band rows.  Returns the number of launches (may exceed cap; entries past 4096 are not
  * recorded), or a negative GOL_E* code. */
 int gol_last_launches(gol_ctx *ctx, int32_t *turns, int32_t *kernel, int32_t *band, int32_t cap);
-/* The same launches' k_step_tile shapes (kernel 15): tile width in lanes, the segment code
- * (SEG + 100 * turn order + 1000 * (words per lane - 1)) and the waves per workgroup; 0 for
- * the other kernels.  Returns the launch count like gol_last_launches. */
+/* The same launches' k_step_tile shapes (kernel 15, and 16 = the same tiles resident across
+ * blocks of turns): tile width in lanes, the segment code (SEG + 100 * turn order + 1000 *
+ * (words per lane - 1)), the waves per workgroup and the turns per block (kernel 15: the
+ * launch's turns); 0 for the other kernels.  Returns the launch count like
+ * gol_last_launches. */
 int gol_last_launch_tiles(gol_ctx *ctx, int32_t *tile_w, int32_t *tile_seg, int32_t *waves,
-                          int32_t cap);
+                          int32_t *block_turns, int32_t cap);
 /* The k_step_tile segment codes this library runs (planner introspection for the parity
  * tests: every code the shape search can pick has an oracle test).  Writes min(n, cap) codes,
  * returns n.  Needs no device. */

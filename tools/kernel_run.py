@@ -2,7 +2,8 @@
 """Run ONE pinned stencil configuration (no create-time autotune) for `--turns` turns, for
 profiler passes that must see only the shipped kernel (rocprofv3 --pmc / --kernel-trace).
 usage: python tools/kernel_run.py --size 65536 --mv 7 --tpl 10 --band 137 --turns 100
-       [--tile TW,SEG]  (mv 15 = k_step_tile, band = tile height)"""
+       [--tile TW,SEG] [--persist K]  (mv 15 = k_step_tile, band = tile height; --persist:
+       the same tiles resident across blocks of K turns, k_tile_persist)"""
 import argparse
 import os
 import sys
@@ -20,11 +21,15 @@ def main():
     ap.add_argument("--tpl", type=int, required=True)
     ap.add_argument("--band", type=int, required=True)
     ap.add_argument("--tile", default="")
+    ap.add_argument("--persist", type=int, default=0,
+                    help="k_tile_persist blocks of this many turns (mv 15 only)")
     ap.add_argument("--turns", type=int, default=100)
     a = ap.parse_args()
     os.environ["GOL_MULTI_VARIANT"] = str(a.mv)
     if a.tile:
         os.environ["GOL_TILE"] = a.tile
+    if a.persist:
+        os.environ["GOL_PERSIST"] = str(a.persist)
     import torch
     import gol
     W, H = a.size, a.height or a.size

@@ -1,0 +1,53 @@
+#!/bin/bash
+# Round-4 profiles that reproduce the bench line: (1) the bench exactly as the driver runs it
+# (bench.py --gpus 1 --steps 20 --warmup 5, all configs) under --kernel-trace --stats; (2) for
+# the headline board, C3 and C2, the launch shape the bench reports (config.launch_shape /
+# configs_measured[i].launch_shape), pinned in tools/kernel_run.py (no autotune), under a
+# FETCH_SIZE pass, a WRITE_SIZE pass and a kernel trace of its own -- so the traffic and the
+# trace average of each summary come from the one instantiation the bench timed.
+# tools/summarize_profile.py then writes profiles/r04_k{K}_{size}_{tag}_summary.json.
+set -u
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd /tmp && export TMPDIR=/tmp
+O="$R/gpurun_out/prof4"
+mkdir -p "$O"
+run() {  # name seconds args...
+  local name=$1 t=$2; shift 2
+  timeout -s KILL "$t" rocprofv3 "$@" > "$O/$name.log" 2>&1
+  local rc=$?; echo "$name rc=$rc"; [ $rc -ne 0 ] && exit $rc; return 0
+}
+run kt 400 --kernel-trace --stats -d "$O/kt" -o run --output-format csv -- \
+    python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+grep '^{"metric"' "$O/kt.log" > "$O/bench_line.json" || { echo "no bench line"; exit 1; }
+# pinned kernel_run arguments per board: "name size turns args..." lines
+python3 - "$O/bench_line.json" > "$O/pins.txt" <<'PY'
+import json, sys
+line = json.load(open(sys.argv[1]))
+boards = [("h", line["config"]["board"][0], line["config"]["launch_shape"])]
+for i, c in enumerate(line.get("configs_measured", [])[:2]):
+    if "launch_shape" in c:
+        size = int(c["workload"].split("x")[0])
+        boards.append((["c3", "c2"][i], size, c["launch_shape"]))
+for name, size, sh in boards:
+    k = sh["turns"]
+    args = f"--size {size} --mv {15 if sh['kernel'] in (15, 16) else sh['kernel']} --band {sh['band_rows']}"
+    if sh["kernel"] == 16:
+        t = sh["tile"]
+        args += f" --tile {t['width_lanes']},{t['code']} --tpl {sh['block_turns']} --persist {sh['block_turns']}"
+    elif sh["kernel"] == 15:
+        t = sh["tile"]
+        args += f" --tile {t['width_lanes']},{t['code']} --tpl {k}"
+    else:
+        args += f" --tpl {k}"
+    turns = k * (10 if size >= 65536 else 40)
+    print(name, size, k, json.dumps(sh, separators=(",", ":")), args, "--turns", turns)
+PY
+cat "$O/pins.txt"
+while read -r name size k shape args; do
+  KR="$R/tools/kernel_run.py $args"
+  run "fetch_$name" 200 --pmc FETCH_SIZE -d "$O/fetch_$name" -o run --output-format csv -- python3 $KR
+  run "write_$name" 200 --pmc WRITE_SIZE -d "$O/write_$name" -o run --output-format csv -- python3 $KR
+  run "ktpin_$name" 200 --kernel-trace --stats -d "$O/ktpin_$name" -o run --output-format csv -- python3 $KR
+  echo "$shape" > "$O/shape_$name.json"
+done < "$O/pins.txt"
+echo done

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 run of bench.py into profiles/<tag>_*.{csv,json}.
 
-Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL]
+Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL] [SHAPE_JSON]
   SRC    the pass directory root (tools/profile_r02.sh: gpurun_out/prof2)
   KT     the --kernel-trace --stats pass (KT/ + KT.log holding the bench line), or - for
          a PMC-only summary
@@ -9,6 +9,7 @@ Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL]
   BOARD  which board of the bench run: 0 = the headline board, 1 = configs_measured[0]
   KERNEL (PMC passes of tools/kernel_run.py, which loads no board): the last 20 dispatches
          whose name contains this text instead of the first board's
+  SHAPE_JSON  the bench's launch_shape that the pinned PMC passes ran (stored as `shape`)
 
 Timed dispatches: bench.py loads each board (k_il_convert), steps the warm-up turns, then
 the timed turns, so the timed launches are the last `launches` stencil dispatches
@@ -44,7 +45,7 @@ def board_segments(rows):
             segs.append(cur)
         elif "k_fill_random" in name:
             cur = None
-        elif cur is not None and "k_step" in name:
+        elif cur is not None and ("k_step" in name or "k_tile_persist" in name):
             cur.append(r)
     return segs
 
@@ -55,11 +56,15 @@ def load_rows(path):
     return rows
 
 
-def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None):
+def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=None):
     board = int(board)
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     res = {"source": f"{os.path.relpath(src, ROOT)}/{kt}", "board": board}
+    if shape:
+        # the launch shape (bench.py launch_shape) the PMC passes pinned: bench.py reports
+        # `traffic` from this summary only for a launch of exactly this shape
+        res["shape"] = json.loads(shape)
     line = None
     if kt != "-":
         shutil.copy(os.path.join(src, kt, "run_kernel_stats.csv"),
