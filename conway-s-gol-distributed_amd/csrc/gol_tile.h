@@ -128,12 +128,19 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     // cells (s[4w], s[4w+1]) and of the odd cells (s[4w+2], s[4w+3]); K1s's stage, with the
     // neighbour words inside the lane taken as they are
     auto rsum = [&](const uint32_t (&x)[ND], uint32_t (&s)[NS]) {
-        const uint32_t L = dpp_from_lower_z(x[ND - 1]);  // west lane's last odd cells
         const uint32_t Rt = dpp_from_upper_z(x[0]);      // east lane's first even cells
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const uint32_t e = x[2 * w], o = x[2 * w + 1];
+#if GOL_TILE_CARRY
+            // (experiment build: the west lane's top odd cell through the carry mask instead
+            // of a DPP move + v_alignbit, gol_device.h shl1_from_lower_lane)
+            const uint32_t wl = w == 0 ? shl1_from_lower_lane(o)
+                                       : __builtin_amdgcn_alignbit(o, x[2 * w - 1], 31);
+#else
+            const uint32_t L = dpp_from_lower_z(x[ND - 1]);   // west lane's last odd cells
             const uint32_t wl = __builtin_amdgcn_alignbit(o, w == 0 ? L : x[2 * w - 1], 31);
+#endif
             const uint32_t er = __builtin_amdgcn_alignbit(w == W - 1 ? Rt : x[2 * w + 2], e, 1);
             s[4 * w + 0] = xor3(wl, e, o);
             s[4 * w + 1] = maj(wl, e, o);
