@@ -757,7 +757,8 @@ def test_tile_persist_pinned(gol, oracle, monkeypatch, code, shape):
         e.step(turns)
         plan = e.last_launches()
         assert [v for _, v, _ in plan] == [16] and plan[0][0] == turns, plan
-        assert e.last_launch_tiles(blocks=True)[0][::2] == (tw, K), e.last_launch_tiles(blocks=True)
+        t = e.last_launch_tiles(blocks=True)[0]
+        assert (t[0], t[1], t[3]) == (tw, code, K), t
         mid = e.read_packed()
         e.step(turns + 3)
         got = e.read_packed()
