@@ -33,27 +33,6 @@ __device__ __forceinline__ uint32_t dpp_from_upper_z(uint32_t v)
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
 }
 
-#ifndef GOL_TILE_CARRY
-#define GOL_TILE_CARRY 0   // 1: the carry-mask west shift in k_step_tile (A/B build, make carry)
-#endif
-// (o << 1) | (bit 31 of o in lane i - 1), lane 0 shifting in 0: the funnel shift of
-// v_alignbit(o, dpp_from_lower_z(o), 31) without its two half-rate instructions -- the add
-// puts each lane's bit 31 in a lane mask, the scalar unit shifts the mask up one lane, and
-// the add-with-carry takes it in.  (s_nop 3: the VALU-written mask settles before the SALU
-// reads it.)
-__device__ __forceinline__ uint32_t shl1_from_lower_lane(uint32_t o)
-{
-    uint32_t t, r;
-    uint64_t c0, c1, c2;
-    asm volatile("v_add_co_u32 %0, %3, %5, %5\n\t"
-                 "s_nop 3\n\t"
-                 "s_lshl_b64 %4, %3, 1\n\t"
-                 "v_addc_co_u32 %1, %2, %0, 0, %4"
-                 : "=&v"(t), "=v"(r), "=&s"(c2), "=&s"(c0), "=&s"(c1)
-                 : "v"(o));
-    return r;
-}
-
 template <typename T>
 __device__ __forceinline__ T maj3(T a, T b, T c) { return (a & b) | (c & (a | b)); }
 

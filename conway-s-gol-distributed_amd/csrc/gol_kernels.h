@@ -195,6 +195,7 @@ constexpr int kTileCodes[] = {
     102,  103,  104,  106,  108,  112,  116,  124,  132,  140,                  // ORD 1
     203,  204,  206,  208,  212,  216,  224,  232,  240,                        // ORD 2
     403,  404,  406,  408,  412,  416,  424,  432,  440,                        // ORD 4
+    503,  504,  506,  508,  512,  516,  524,  532,  540,                        // ORD 5
     1002, 1003, 1004, 1006, 1008,                                               // W 2
     1102, 1103, 1104, 1106, 1108,
     1204, 1206, 1208,
@@ -202,7 +203,9 @@ constexpr int kTileCodes[] = {
 // the codes k_tile_persist (K1p) is instantiated for (gol_tile.hip persist_fn; each pinned by
 // tests/test_gpu_engine.py::test_tile_persist_pinned through gol_tile_persist_codes)
 constexpr int kTilePersistCodes[] = {102, 103, 104, 106, 108, 112, 116,
-                                     403, 404, 406, 408, 412, 416};
+                                     403, 404, 406, 408, 412, 416,
+                                     2, 3, 4, 6, 8,
+                                     503, 504, 506, 508};
 constexpr bool tile_code_shipped(int code)
 {
     for (int c : kTileCodes)

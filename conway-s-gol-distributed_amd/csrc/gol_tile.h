@@ -51,7 +51,8 @@ constexpr size_t tile_lds_bytes(int threads, int words)
 // tile_seg = SEG + 100 * ORD + 1000 * (W - 1): rows per lane segment, turn order (0: in order;
 // 1: interior rows, then the edge rows; 2: the same with the barrier after the interior rows;
 // 4: ORD 1 with no workgroup barrier -- each wave waits only for its two neighbour waves'
-// published edge sums, through per-wave progress flags in LDS), words per lane
+// published edge sums, through per-wave progress flags in LDS; 5: ORD 1 with the edge sums
+// read back from LDS instead of kept in registers), words per lane
 constexpr int tile_seg_rows(int code) { return code % 100; }
 constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 
@@ -132,15 +133,8 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const uint32_t e = x[2 * w], o = x[2 * w + 1];
-#if GOL_TILE_CARRY
-            // (experiment build: the west lane's top odd cell through the carry mask instead
-            // of a DPP move + v_alignbit, gol_device.h shl1_from_lower_lane)
-            const uint32_t wl = w == 0 ? shl1_from_lower_lane(o)
-                                       : __builtin_amdgcn_alignbit(o, x[2 * w - 1], 31);
-#else
             const uint32_t L = dpp_from_lower_z(x[ND - 1]);   // west lane's last odd cells
             const uint32_t wl = __builtin_amdgcn_alignbit(o, w == 0 ? L : x[2 * w - 1], 31);
-#endif
             const uint32_t er = __builtin_amdgcn_alignbit(w == W - 1 ? Rt : x[2 * w + 2], e, 1);
             s[4 * w + 0] = xor3(wl, e, o);
             s[4 * w + 1] = maj(wl, e, o);
@@ -241,7 +235,10 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     };
     // ORD 4's turn: the edge sums F (row 0) and Lr (row SEG-1) go to LDS and are read back
     // from the wave's own slots when needed, instead of staying live across the interior rows
-    // and the wait (64 VGPRs at SEG 16: 8 waves per SIMD)
+    // and the wait (64 VGPRs at SEG 16: 8 waves per SIMD).  ORD 5: the same turn with ORD 1's
+    // workgroup barrier after the puts instead of the flags (80 VGPRs at SEG 24: 6 waves per
+    // SIMD, where the stencil's instruction mix issues fastest -- tools/calib/valu_issue.hip
+    // occupancy sweep)
     auto turn4 = [&](auto P, int poff, int t) {
         constexpr int p = decltype(P)::value;
         const int off = poff;
@@ -252,7 +249,8 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             rsum(v[SEG - 1], Lr);
             put(wtop(p, off), F);
             put(wbot(p, off), Lr);
-            publish(t);
+            if constexpr (ORD == 5) __syncthreads();
+            else publish(t);
 #pragma unroll
             for (int k = 0; k < NS; ++k) Pw[k] = F[k];
         }
@@ -287,7 +285,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         rule(Pw, F, D, v[SEG - 1]);
     };
     auto turn = [&](auto P, int poff, int t) {
-        if constexpr (ORD == 4) {
+        if constexpr (ORD == 4 || ORD == 5) {
             turn4(P, poff, t);
             return;
         }

@@ -30,11 +30,11 @@ static void *tile_fn(int seg)
     }
 }
 
-// k_tile_persist instantiations (K1p, small boards): one word per lane, interior rows first
-// with the workgroup barrier (ORD 1) or with neighbour flags (ORD 4), SEG 2..16
+// k_tile_persist instantiations (K1p, small boards): one word per lane; in order (ORD 0),
+// interior rows first with the workgroup barrier (ORD 1, 5) or with neighbour flags (ORD 4)
 static void *persist_fn(int code)
 {
-    static_assert(std::size(kTilePersistCodes) == 13, "persist_fn covers kTilePersistCodes");
+    static_assert(std::size(kTilePersistCodes) == 22, "persist_fn covers kTilePersistCodes");
     switch (code) {
     case 102: return reinterpret_cast<void *>(&k_tile_persist<2, 1, 1>);
     case 103: return reinterpret_cast<void *>(&k_tile_persist<3, 1, 1>);
@@ -49,6 +49,15 @@ static void *persist_fn(int code)
     case 408: return reinterpret_cast<void *>(&k_tile_persist<8, 4, 1>);
     case 412: return reinterpret_cast<void *>(&k_tile_persist<12, 4, 1>);
     case 416: return reinterpret_cast<void *>(&k_tile_persist<16, 4, 1>);
+    case 2: return reinterpret_cast<void *>(&k_tile_persist<2, 0, 1>);
+    case 3: return reinterpret_cast<void *>(&k_tile_persist<3, 0, 1>);
+    case 4: return reinterpret_cast<void *>(&k_tile_persist<4, 0, 1>);
+    case 6: return reinterpret_cast<void *>(&k_tile_persist<6, 0, 1>);
+    case 8: return reinterpret_cast<void *>(&k_tile_persist<8, 0, 1>);
+    case 503: return reinterpret_cast<void *>(&k_tile_persist<3, 5, 1>);
+    case 504: return reinterpret_cast<void *>(&k_tile_persist<4, 5, 1>);
+    case 506: return reinterpret_cast<void *>(&k_tile_persist<6, 5, 1>);
+    case 508: return reinterpret_cast<void *>(&k_tile_persist<8, 5, 1>);
     default: return nullptr;
     }
 }
@@ -61,6 +70,7 @@ void *tile_kernel(int code)
 #endif
     if (code < 0 || w > 2) return nullptr;
     if (ord == 4) return w == 1 && seg >= 3 && seg <= 40 ? tile_fn<4, 1>(seg) : nullptr;
+    if (ord == 5) return w == 1 && seg >= 3 && seg <= 40 ? tile_fn<5, 1>(seg) : nullptr;
     if (ord > 2) return nullptr;
     if (w == 2) return ord == 2 ? tile_fn<2, 2>(seg) : ord ? tile_fn<1, 2>(seg) : tile_fn<0, 2>(seg);
     return ord == 2 ? tile_fn<2, 1>(seg) : ord ? tile_fn<1, 1>(seg) : tile_fn<0, 1>(seg);

@@ -25,13 +25,15 @@ TILE_CODES = (2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
               102, 103, 104, 106, 108, 112, 116, 124, 132, 140,
               203, 204, 206, 208, 212, 216, 224, 232, 240,
               403, 404, 406, 408, 412, 416, 424, 432, 440,
+              503, 504, 506, 508, 512, 516, 524, 532, 540,
               1002, 1003, 1004, 1006, 1008,
               1102, 1103, 1104, 1106, 1108,
               1204, 1206, 1208)
 
 
 # the subset the persistent tile kernel (K1p) runs (gol_tile_persist_codes)
-TILE_PERSIST_CODES = (102, 103, 104, 106, 108, 112, 116, 403, 404, 406, 408, 412, 416)
+TILE_PERSIST_CODES = (102, 103, 104, 106, 108, 112, 116, 403, 404, 406, 408, 412, 416,
+                      2, 3, 4, 6, 8, 503, 504, 506, 508)
 
 
 def pytest_configure(config):
