@@ -107,15 +107,19 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     const __amdgpu_buffer_rsrc_t rout =
         __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)span, kBufFlags);
 
+    // PERSIST: loads bypass this CU's vector L1 (sc1): block b reads rows other CUs wrote
+    // since block b - 2 left lines of the same buffer in it, and the L1 is never refreshed
+    // by another CU's stores
+    constexpr int kLoadAux = PERSIST ? 16 : 0;
     uint32_t v[SEG][ND];
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
         if constexpr (W == 1) {
-            const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, 0);
+            const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, kLoadAux);
             v[i][0] = w.x;
             v[i][1] = w.y;
         } else {
-            const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+            const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kLoadAux);
             v[i][0] = w.x;
             v[i][1] = w.y;
             v[i][2] = w.z;
@@ -452,7 +456,8 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
 // is one tile_pass; between blocks a tile exchanges its borders with its 8 neighbours through
 // memory instead of ending the launch: block b reads buffer u[(b-1) % 2] (block 0: `in`) and
 // writes u[b % 2] (the last block: `out`); u0 / u1 are uncached (visible across the XCDs' L2s
-// without cache maintenance, like the k_step_wg parallelogram rows).  flags[tile] = epoch + b
+// without cache maintenance, like the k_step_wg parallelogram rows) and read with sc1 loads
+// that bypass the CU's vector L1.  flags[tile] = epoch + b
 // + 1 once the tile's block-b stores completed; a tile starts block b when its 8 neighbours
 // are there -- which also means they finished reading the buffer it is about to overwrite.
 // A wait that gives up after kTileSpinLimit polls marks the error word (GOL_EHIP at the next
@@ -500,9 +505,11 @@ __global__ __launch_bounds__(1024, 1) void k_tile_persist(
         if (b + 1 == nblocks) break;
         __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // this wave's stores are done
         __syncthreads();                                     // ... and every wave's
+        // (u0 / u1 are uncached: completed stores are in memory; the flag is an agent-scope
+        // store, a workgroup-scope release would order nothing across CUs)
         if (threadIdx.x == 0)
-            __hip_atomic_store(flags + tile, epoch + (unsigned)b + 1u, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(flags + tile, epoch + (unsigned)b + 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     if (gave_up && a.err)
         __hip_atomic_store(a.err, kDevErrTileFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
