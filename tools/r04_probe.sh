@@ -2,9 +2,8 @@
 # Round-4 probes on one GPU box (each step has its own limit; a failing step ends the script).
 #   PART=tests : the round's new GPU tests + the C2 (5120^2) autotune with and without K1p
 #   PART=perf  : the stencil mix's issue rate at every occupancy; 65536^2 tile shapes at
-#                K = 20 with the barrier (ORD 1) and with neighbour flags (ORD 4); the
-#                carry-mask west-shift build (libgolamd_carry.so) on the same shapes + parity;
-#                SQ counter passes of the two main shapes (PMC=1)
+#                K = 20 with the barrier (ORD 1) and with neighbour flags (ORD 4); SQ
+#                counter passes of the two main shapes (PMC=1)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
@@ -24,8 +23,6 @@ if [ "${PART:-all}" != tests ]; then
   step calib_occ 120 tools/calib/valu_issue 20000 occupancy
   SHAPES=${SHAPES:-14:984:116:20,14:984:416:20,30:472:116:20,30:472:416:20,30:600:140:20,30:600:440:20,30:536:124:20,30:536:424:20,30:1240:140:20,30:1240:440:20,62:600:140:20,62:600:440:20}
   step sweep65c 400 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes "$SHAPES"
-  step carry_parity 300 env GOL_AMD_LIB=$PWD/$B/libgolamd_carry.so python -u -m pytest tests/test_gpu_engine.py -x -q --timeout 150 --timeout-method thread -k "tile_code_pinned and (103 or 104 or 116 or 140 or 416 or 440 or 1008 or 206)"
-  step carry_sweep 300 env GOL_AMD_LIB=$PWD/$B/libgolamd_carry.so python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 14:984:416:20,30:600:140:20,30:600:440:20,30:1240:140:20
   if [ -n "${PMC:-}" ]; then
     step pmc_s16 200 env TAG=_s16 bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 20 --band 984 --tile 14,416 --turns 100
     step pmc_s40 200 env TAG=_s40 bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 20 --band 600 --tile 30,140 --turns 100
