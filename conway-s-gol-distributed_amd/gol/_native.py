@@ -105,6 +105,7 @@ SIGNATURES = {
     "gol_destroy": (None, [_vp]),
     "gol_last_error": (ctypes.c_char_p, [_vp]),
     "gol_strerror": (ctypes.c_char_p, [_i32]),
+    "gol_source_id": (ctypes.c_char_p, []),
     "gol_get_info": (_i32, [_vp, ctypes.POINTER(gol_info)]),
     "gol_set_stream": (_i32, [_vp, _vp]),
     "gol_get_stream": (_vp, [_vp]),

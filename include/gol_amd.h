@@ -113,6 +113,9 @@ int  gol_create_ex(const gol_config *cfg, gol_ctx **out);
 void gol_destroy(gol_ctx *ctx);
 const char *gol_last_error(const gol_ctx *ctx);   /* per engine; "" if none            */
 const char *gol_strerror(int code);
+/* Build stamp: 16 hex digits of the sha256 of the library's sources (csrc/Makefile SRCS), so
+ * a test can tell a library built from other sources than the tree it ships with. */
+const char *gol_source_id(void);
 int  gol_get_info(gol_ctx *ctx, gol_info *info);
 
 /* Stream: the engine creates its own HIP stream; gol_set_stream makes it enqueue

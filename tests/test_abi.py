@@ -3,6 +3,7 @@ No compute calls here (no GPU in the build container)."""
 import ctypes
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -19,6 +20,49 @@ def test_header_symbols_exported():
                         text=True, check=True).stdout
     exported = {line.split()[-1] for line in nm.splitlines() if " T " in line}
     assert set(declared) <= exported
+
+
+def _tree_source_id():
+    """csrc/Makefile's SRCS hash, recomputed from the tree."""
+    import glob
+    import hashlib
+    from gol import _native as N
+    csrc = os.path.join(os.path.dirname(os.path.dirname(N.LIB_PATH)), "csrc")
+    files = sorted(os.path.basename(f) for e in ("hip", "h", "cpp")
+                   for f in glob.glob(os.path.join(csrc, "*." + e)))
+    files = [os.path.join(csrc, f) for f in files] + [N.HEADER_PATH, os.path.join(csrc, "Makefile")]
+    h = hashlib.sha256()
+    for f in files:
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def _check_libraries_match_sources():
+    from gol import _native as N
+    want = _tree_source_id()
+    assert N.lib().gol_source_id().decode() == want, "libgolamd.so is stale: rebuild (make -C csrc)"
+    build = os.path.dirname(N.LIB_PATH)
+    for extra in ("libgolamd_spin0.so",):
+        p = os.path.join(build, extra)
+        if os.path.exists(p):
+            # (in a child: two copies of the library in one process would share nothing, but
+            # a child keeps the test's own process clean)
+            code = ("import ctypes,sys; L=ctypes.CDLL(sys.argv[1]); "
+                    "L.gol_source_id.restype=ctypes.c_char_p; print(L.gol_source_id().decode())")
+            got = subprocess.run([sys.executable, "-c", code, p], capture_output=True,
+                                 text=True, check=True).stdout.strip()
+            assert got == want, f"{extra} is stale"
+
+
+def test_libraries_match_sources():
+    """The shipped libraries were built from the sources in this tree (gol_source_id)."""
+    _check_libraries_match_sources()
+
+
+@pytest.mark.gpu
+def test_libraries_match_sources_on_box():
+    """Same check on the GPU box: the binaries the GPU tests load match the pushed tree."""
+    _check_libraries_match_sources()
 
 
 def test_tile_codes_are_the_pinned_list():
