@@ -672,7 +672,8 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     }
     static constexpr int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
                                      106, 108, 112, 116, 124, 132, 140,
-                                     203, 204, 206, 208, 212, 216, 224, 232, 240};
+                                     203, 204, 206, 208, 212, 216, 224, 232, 240,
+                                     506, 512, 516, 524};
     static constexpr int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1106, 1108, 1204, 1206, 1208};
     static_assert(all_shipped(kSegs1) && all_shipped(kSegs2), "a tile code outside kTileCodes");
     std::vector<int> segs = W == 1 ? std::vector<int>(std::begin(kSegs1), std::end(kSegs1))
@@ -786,6 +787,17 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         for (int sg : kShort)
             for (int tw : {14, tws.empty() ? 14 : tws[0]})
                 for (int wv : {8, 16}) improve(P{base.K, wv, tw, sg});
+        // ... and the 80-VGPR family: ORD 5 (edge sums read back from LDS) at SEG 16-24 holds
+        // 6 waves per SIMD -- two 12-wave workgroups per CU, the occupancy at which the
+        // stencil's instruction mix issues fastest (tools/calib/valu_issue occupancy: 1.66
+        // cycles per instruction against 2.43 at 4 waves); 30 x 536 tiles of SEG 24 ran 34.6
+        // us per turn at 65536^2 against 36.3 for the best 4-wave shape
+        // (profiles/r04_sweep_65536_ord5.log)
+        static constexpr int kSix[] = {524, 516};
+        static_assert(all_shipped(kSix), "a tile code outside kTileCodes");
+        for (int sg : kSix)
+            for (int tw : {tws.empty() ? 30 : tws[0], 14})
+                for (int wv : {12, 8}) improve(P{base.K, wv, tw, sg});
     }
     {
         const P base = cur;
@@ -880,9 +892,14 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
 void persist_tune(gol_ctx *c)
 {
     c->persist_k = 0;
+    const bool log = getenv("GOL_AUTOTUNE_LOG") != nullptr;
     if (is_strip(c) || c->multi_variant != golk::kMultiTile || !device_exclusive(c->device) ||
-        getenv("GOL_NO_PERSIST"))
+        getenv("GOL_NO_PERSIST")) {
+        if (log)
+            fprintf(stderr, "autotune persist skipped (strip %d variant %d exclusive %d)\n",
+                    (int)is_strip(c), c->multi_variant, (int)device_exclusive(c->device));
         return;
+    }
     golk::StepArgs a{};
     a.width = c->cfg.width;
     a.nw = c->nw;
@@ -927,14 +944,18 @@ void persist_tune(gol_ctx *c)
     int best_k = 0;
     for (int Kp : {c->tpl, 8, 12, 16, 20, 24, 32}) {
         if (Kp < 2 || !golk::tile_persist_ok(c->nw, c->buf_rows, N, Kp, c->band_multi, c->tile_w,
-                                             c->tile_seg, c->ncu))
+                                             c->tile_seg, c->ncu)) {
+            if (log)
+                fprintf(stderr, "autotune persist K=%d: shape %d:%d:%d not persistent-capable\n",
+                        Kp, c->tile_w, c->band_multi, c->tile_seg);
             continue;
+        }
         const float us = timed([&]() {
             a.in = c->board[0];
             a.out = c->board[1];
             return persist_launch(c, a, N, Kp) == hipSuccess;
         });
-        if (getenv("GOL_AUTOTUNE_LOG"))
+        if (log)
             fprintf(stderr, "autotune persist %dx%d K=%d us_per_turn=%.4f (plain K=%d %.4f)\n",
                     c->cfg.width, c->buf_rows, Kp, us, c->tpl, plain);
         if (us > 0.f && (best == 0.f || us < best)) {
