@@ -940,27 +940,37 @@ void persist_tune(gol_ctx *c)
         }
         return true;
     });
+    // the tuned code and its siblings with the same rows per segment (K1p is instantiated for
+    // ORD 0, 1, 4 and 5 only: an ORD 2 pick runs persistent as one of those)
     float best = 0.f;
-    int best_k = 0;
-    for (int Kp : {c->tpl, 8, 12, 16, 20, 24, 32}) {
-        if (Kp < 2 || !golk::tile_persist_ok(c->nw, c->buf_rows, N, Kp, c->band_multi, c->tile_w,
-                                             c->tile_seg, c->ncu)) {
+    int best_k = 0, best_code = 0;
+    const int sg = c->tile_seg % 100;
+    const int codes[] = {c->tile_seg, 100 + sg, 500 + sg, 400 + sg, sg};
+    for (int ci = 0; ci < (int)std::size(codes); ++ci) {
+        const int code = codes[ci];
+        if (c->tile_seg >= 1000 || (ci > 0 && code == c->tile_seg)) continue;   // (W = 1 only)
+        a.tile_seg = code;
+        for (int Kp : {c->tpl, 8, 12, 16, 20, 24, 32}) {
+            if (Kp < 2 || !golk::tile_persist_ok(c->nw, c->buf_rows, N, Kp, c->band_multi,
+                                                 c->tile_w, code, c->ncu)) {
+                if (log)
+                    fprintf(stderr, "autotune persist K=%d: shape %d:%d:%d not persistent-capable\n",
+                            Kp, c->tile_w, c->band_multi, code);
+                continue;
+            }
+            const float us = timed([&]() {
+                a.in = c->board[0];
+                a.out = c->board[1];
+                return persist_launch(c, a, N, Kp) == hipSuccess;
+            });
             if (log)
-                fprintf(stderr, "autotune persist K=%d: shape %d:%d:%d not persistent-capable\n",
-                        Kp, c->tile_w, c->band_multi, c->tile_seg);
-            continue;
-        }
-        const float us = timed([&]() {
-            a.in = c->board[0];
-            a.out = c->board[1];
-            return persist_launch(c, a, N, Kp) == hipSuccess;
-        });
-        if (log)
-            fprintf(stderr, "autotune persist %dx%d K=%d us_per_turn=%.4f (plain K=%d %.4f)\n",
-                    c->cfg.width, c->buf_rows, Kp, us, c->tpl, plain);
-        if (us > 0.f && (best == 0.f || us < best)) {
-            best = us;
-            best_k = Kp;
+                fprintf(stderr, "autotune persist %dx%d code=%d K=%d us_per_turn=%.4f (plain K=%d %.4f)\n",
+                        c->cfg.width, c->buf_rows, code, Kp, us, c->tpl, plain);
+            if (us > 0.f && (best == 0.f || us < best)) {
+                best = us;
+                best_k = Kp;
+                best_code = code;
+            }
         }
     }
     (void)hipEventDestroy(e0);
@@ -972,6 +982,7 @@ void persist_tune(gol_ctx *c)
     if (bad) clear_dev_err(c);
     if (best > 0.f && plain > 0.f && best < 0.98f * plain && !bad) {
         c->persist_k = best_k;
+        c->tile_seg = best_code;             // (short steps run plain launches of this code)
         c->tuned_us_per_turn = best;
     }
 }
