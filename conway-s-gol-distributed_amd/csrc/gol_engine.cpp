@@ -673,7 +673,7 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     static constexpr int kSegs1[] = {2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
                                      106, 108, 112, 116, 124, 132, 140,
                                      203, 204, 206, 208, 212, 216, 224, 232, 240,
-                                     506, 512, 516, 524};
+                                     506, 512, 516, 524, 612, 616, 624};
     static constexpr int kSegs2[] = {1002, 1003, 1004, 1006, 1008, 1106, 1108, 1204, 1206, 1208};
     static_assert(all_shipped(kSegs1) && all_shipped(kSegs2), "a tile code outside kTileCodes");
     std::vector<int> segs = W == 1 ? std::vector<int>(std::begin(kSegs1), std::end(kSegs1))
@@ -793,7 +793,7 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         // cycles per instruction against 2.43 at 4 waves); 30 x 536 tiles of SEG 24 ran 34.6
         // us per turn at 65536^2 against 36.3 for the best 4-wave shape
         // (profiles/r04_sweep_65536_ord5.log)
-        static constexpr int kSix[] = {524, 516};
+        static constexpr int kSix[] = {524, 624, 516, 616};
         static_assert(all_shipped(kSix), "a tile code outside kTileCodes");
         for (int sg : kSix)
             for (int tw : {tws.empty() ? 30 : tws[0], 14})

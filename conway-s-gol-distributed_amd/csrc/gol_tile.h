@@ -52,7 +52,8 @@ constexpr size_t tile_lds_bytes(int threads, int words)
 // 1: interior rows, then the edge rows; 2: the same with the barrier after the interior rows;
 // 4: ORD 1 with no workgroup barrier -- each wave waits only for its two neighbour waves'
 // published edge sums, through per-wave progress flags in LDS; 5: ORD 1 with the edge sums
-// read back from LDS instead of kept in registers), words per lane
+// read back from LDS instead of kept in registers; 6: ORD 5 with the barrier after the
+// interior rows), words per lane
 constexpr int tile_seg_rows(int code) { return code % 100; }
 constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 
@@ -242,7 +243,9 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     // and the wait (64 VGPRs at SEG 16: 8 waves per SIMD).  ORD 5: the same turn with ORD 1's
     // workgroup barrier after the puts instead of the flags (80 VGPRs at SEG 24: 6 waves per
     // SIMD, where the stencil's instruction mix issues fastest -- tools/calib/valu_issue.hip
-    // occupancy sweep)
+    // occupancy sweep).  ORD 6: the barrier where ORD 4 waits, after the interior rows (ORD
+    // 2's placement: a wave that arrives early has done all the work that needs no neighbour;
+    // the turn-parity double buffer still needs only the one barrier per turn)
     auto turn4 = [&](auto P, int poff, int t) {
         constexpr int p = decltype(P)::value;
         const int off = poff;
@@ -254,7 +257,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             put(wtop(p, off), F);
             put(wbot(p, off), Lr);
             if constexpr (ORD == 5) __syncthreads();
-            else publish(t);
+            else if constexpr (ORD == 4) publish(t);
 #pragma unroll
             for (int k = 0; k < NS; ++k) Pw[k] = F[k];
         }
@@ -279,7 +282,8 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         for (int i = 1; i + 1 < SEG; ++i)
 #pragma unroll
             for (int d = 0; d < ND; ++d) asm volatile("" : "+v"(v[i][d]));
-        await_neighbours(t);
+        if constexpr (ORD == 6) __syncthreads();
+        else await_neighbours(t);
         uint32_t U[NS], D[NS], F[NS];
         get(rup(p, off), U);
         get(wtop(p, off), F);
@@ -289,7 +293,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         rule(Pw, F, D, v[SEG - 1]);
     };
     auto turn = [&](auto P, int poff, int t) {
-        if constexpr (ORD == 4 || ORD == 5) {
+        if constexpr (ORD >= 4) {
             turn4(P, poff, t);
             return;
         }

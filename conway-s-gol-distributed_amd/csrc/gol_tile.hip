@@ -62,6 +62,18 @@ static void *persist_fn(int code)
     }
 }
 
+// ORD 6 (the barrier after the interior rows, edge sums read back): the 6-8 waves per SIMD
+// segments only
+static void *tile_fn6(int seg)
+{
+    switch (seg) {
+    case 12: return reinterpret_cast<void *>(&k_step_tile<12, 6, 1>);
+    case 16: return reinterpret_cast<void *>(&k_step_tile<16, 6, 1>);
+    case 24: return reinterpret_cast<void *>(&k_step_tile<24, 6, 1>);
+    default: return nullptr;
+    }
+}
+
 void *tile_kernel(int code)
 {
     const int seg = code % 100, ord = (code / 100) % 10, w = tile_seg_words(code);
@@ -71,6 +83,7 @@ void *tile_kernel(int code)
     if (code < 0 || w > 2) return nullptr;
     if (ord == 4) return w == 1 && seg >= 3 && seg <= 40 ? tile_fn<4, 1>(seg) : nullptr;
     if (ord == 5) return w == 1 && seg >= 3 && seg <= 40 ? tile_fn<5, 1>(seg) : nullptr;
+    if (ord == 6) return w == 1 ? tile_fn6(seg) : nullptr;
     if (ord > 2) return nullptr;
     if (w == 2) return ord == 2 ? tile_fn<2, 2>(seg) : ord ? tile_fn<1, 2>(seg) : tile_fn<0, 2>(seg);
     return ord == 2 ? tile_fn<2, 1>(seg) : ord ? tile_fn<1, 1>(seg) : tile_fn<0, 1>(seg);
