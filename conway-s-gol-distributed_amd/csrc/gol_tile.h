@@ -37,9 +37,6 @@
 #ifndef GOL_TILE_PAIRS_MAX   // (experiments: the longest segment that runs turns in pairs)
 #define GOL_TILE_PAIRS_MAX 12
 #endif
-#ifndef GOL_TILE_PRIO        // (A/B build: wave priority falls as a wave gets through its turn)
-#define GOL_TILE_PRIO 0
-#endif
 
 namespace golk {
 
@@ -261,7 +258,6 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             put(wbot(p, off), Lr);
             if constexpr (ORD == 5) __syncthreads();
             else if constexpr (ORD == 4) publish(t);
-            if constexpr (GOL_TILE_PRIO) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
             for (int k = 0; k < NS; ++k) Pw[k] = F[k];
         }
@@ -274,10 +270,6 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             if (i + 2 == SEG) get(wbot(p, off), R);   // (own bottom slot: Lr)
             else rsum(v[i + 1], R);
             rule(Pw, Q, R, v[i]);
-            if constexpr (GOL_TILE_PRIO) {
-                if (i == SEG / 3) __builtin_amdgcn_s_setprio(2);
-                if (i == 2 * SEG / 3) __builtin_amdgcn_s_setprio(1);
-            }
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
                 Pw[k] = Q[k];
@@ -299,7 +291,6 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         get(rdn(p, off), D);
         get(wbot(p, off), F);                                 // (Lr)
         rule(Pw, F, D, v[SEG - 1]);
-        if constexpr (GOL_TILE_PRIO) __builtin_amdgcn_s_setprio(0);
     };
     auto turn = [&](auto P, int poff, int t) {
         if constexpr (ORD >= 4) {

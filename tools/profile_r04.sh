@@ -3,8 +3,9 @@
 # (bench.py --gpus 1 --steps 20 --warmup 5, all configs) under --kernel-trace --stats; (2) for
 # the headline board, C3 and C2, the launch shape the bench reports (config.launch_shape /
 # configs_measured[i].launch_shape), pinned in tools/kernel_run.py (no autotune), under a
-# FETCH_SIZE pass, a WRITE_SIZE pass and a kernel trace of its own -- so the traffic and the
-# trace average of each summary come from the one instantiation the bench timed.
+# FETCH_SIZE pass, a WRITE_SIZE pass, a kernel trace and an SQ / GRBM pass (clock under load,
+# VALU counts) of its own -- so the traffic, the clock and the trace average of each summary
+# come from the one instantiation the bench timed.
 # tools/summarize_profile.py then writes profiles/r04_k{K}_{size}_{tag}_summary.json.
 set -u
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -48,6 +49,7 @@ while read -r name size k shape args; do
   run "fetch_$name" 200 --pmc FETCH_SIZE -d "$O/fetch_$name" -o run --output-format csv -- python3 $KR
   run "write_$name" 200 --pmc WRITE_SIZE -d "$O/write_$name" -o run --output-format csv -- python3 $KR
   run "ktpin_$name" 200 --kernel-trace --stats -d "$O/ktpin_$name" -o run --output-format csv -- python3 $KR
+  run "sq_$name" 200 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$O/sq_$name" -o run --output-format csv -- python3 $KR
   echo "$shape" > "$O/shape_$name.json"
 done < "$O/pins.txt"
 echo done

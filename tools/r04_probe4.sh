@@ -8,6 +8,8 @@ step() { local name=$1 t=$2; shift 2
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
   echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log"
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc; }
+step ord6_parity 200 python -u -m pytest tests/test_gpu_engine.py -q --timeout 150 --timeout-method thread -k "tile_code_pinned and (612 or 616 or 624)"
+step sweep65f 400 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 30:536:524:20,30:536:624:20,14:720:624:24,14:720:524:24,30:336:624:24,30:336:524:24,30:472:616:20,14:984:616:20
 step c2_auto 200 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --rounds 3
 step pmc_o5 300 env TAG=_o5 bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 20 --band 536 --tile 30,524 --turns 100
 step pmc_o5n 300 env TAG=_o5n bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 24 --band 720 --tile 14,524 --turns 96

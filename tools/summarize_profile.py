@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 run of bench.py into profiles/<tag>_*.{csv,json}.
 
-Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL] [SHAPE_JSON]
+Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL] [SHAPE_JSON] [SQ]
   SRC    the pass directory root (tools/profile_r02.sh: gpurun_out/prof2)
   KT     the --kernel-trace --stats pass (KT/ + KT.log holding the bench line), or - for
          a PMC-only summary
@@ -10,6 +10,8 @@ Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL] [SHAPE_JSO
   KERNEL (PMC passes of tools/kernel_run.py, which loads no board): the last 20 dispatches
          whose name contains this text instead of the first board's
   SHAPE_JSON  the bench's launch_shape that the pinned PMC passes ran (stored as `shape`)
+  SQ     a --pmc pass of GRBM_GUI_ACTIVE + SQ_* counters of the same pinned run: the clock
+         under load (GRBM_GUI_ACTIVE / 8 XCDs / dispatch duration) and the VALU counts
 
 Timed dispatches: bench.py loads each board (k_il_convert), steps the warm-up turns, then
 the timed turns, so the timed launches are the last `launches` stencil dispatches
@@ -56,7 +58,7 @@ def load_rows(path):
     return rows
 
 
-def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=None):
+def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=None, sq=None):
     board = int(board)
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -109,6 +111,25 @@ def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=Non
         res["read_bytes_per_launch"] = rd
         res["write_bytes_per_launch"] = wr
         res["traffic_bytes_per_launch"] = rd + wr
+    if sq and sq != "-":
+        rows = load_rows(os.path.join(src, sq, "run_counter_collection.csv"))
+        if kernel:
+            rows = [r for r in rows if kernel in r["Kernel_Name"]]
+        else:
+            rows = board_segments(rows)[0]
+        by, dur = {}, {}
+        for r in rows:
+            by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        med = {n: statistics.median(v[-20:]) for n, v in by.items()}
+        us = statistics.median(list(dur.values())[-20:])
+        res["sq_counters_median"] = med
+        res["sq_dispatch_us_median"] = us
+        if "GRBM_GUI_ACTIVE" in med:
+            res["clock_ghz"] = round(med["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3), 4)
+        if "SQ_ACTIVE_INST_VALU" in med and "SQ_WAVE_CYCLES" in med:
+            res["valu_active_per_wave_cycle"] = round(med["SQ_ACTIVE_INST_VALU"] /
+                                                      med["SQ_WAVE_CYCLES"], 4)
     with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
         json.dump(res, f, indent=1)
     show = {k: v for k, v in res.items() if k != "bench_line"}
