@@ -102,12 +102,12 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(size, k, shape=None):
-    """HBM traffic per launch of the stencil from the newest committed rocprofv3 PMC pass
-    for this board size, depth k and -- when the summary records one -- launch shape
-    (profiles/rNN_k{k}_{size}*_summary.json, written by tools/profile.sh +
-    tools/summarize_profile.py): a summary whose `shape` differs from the launch that ran is
-    not used, so `traffic` always comes from the kernel the bench timed.  None if no pass."""
+def pmc_summary(size, k, shape=None):
+    """The newest committed rocprofv3 PMC summary for this board size, depth k and -- when the
+    summary records one -- launch shape (profiles/rNN_k{k}_{size}*_summary.json, written by
+    tools/profile_r04.sh + tools/summarize_profile.py): a summary whose `shape` differs from
+    the launch that ran is not used, so `traffic` (and the clock under load) always come from
+    the kernel the bench timed.  (None, None) if no pass."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_k{k}_{size}*_summary.json")))
     for path in reversed(files):                 # the newest pass that holds PMC bytes
@@ -119,8 +119,14 @@ def pmc_traffic(size, k, shape=None):
             continue
         if "shape" not in d and shape is not None and shape.get("kernel") == 15:
             continue                             # (older passes: shape unknown)
-        return d["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+        return d, os.path.relpath(path, ROOT)
     return None, None
+
+
+def pmc_traffic(size, k, shape=None):
+    """HBM traffic per launch of the stencil from pmc_summary; (None, None) if no pass."""
+    d, src = pmc_summary(size, k, shape)
+    return (d["traffic_bytes_per_launch"], src) if d else (None, None)
 
 
 def cpu_share():
@@ -495,7 +501,17 @@ def main():
                 "unit": "GCUPS per GPU", "frac": round(per_gpu / VALU_PEAK_GCUPS, 4),
                 "model": "52 SIMD cycles per 4096 cell-updates (18 full-rate v_bitop3 + 4 "
                          "half-rate v_alignbit/DPP), 1024 SIMDs x 2.4 GHz; useful cell-updates "
-                         "only (halo lanes, band halos and pipeline fill count against it)"}
+                         "only (halo lanes, band halos and pipeline fill count against it)",
+                "clock_ghz_measured": None, "peak_at_measured_clock": None,
+                "frac_at_measured_clock": None, "clock_source": None}
+            d, src = pmc_summary(W, kdepth, shape)
+            if d and d.get("clock_ghz"):
+                # the same model at the clock the kernel ran at under load (GRBM_GUI_ACTIVE
+                # per XCD over the dispatch time, the SQ pass of the pinned shape)
+                pk = VALU_PEAK_GCUPS * d["clock_ghz"] / (VALU_CLOCK_HZ / 1e9)
+                out["valu_roofline"].update({
+                    "clock_ghz_measured": d["clock_ghz"], "peak_at_measured_clock": round(pk, 1),
+                    "frac_at_measured_clock": round(per_gpu / pk, 4), "clock_source": src})
         if world > 1:
             out["config"]["exchanges_timed"] = m["exchanges"]
         cm = []
