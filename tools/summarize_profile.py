@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 run of bench.py into profiles/<tag>_*.{csv,json}.
 
-Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL] [SHAPE_JSON] [SQ]
+Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL] [SHAPE_JSON] [SQ] [KTPIN]
   SRC    the pass directory root (tools/profile_r02.sh: gpurun_out/prof2)
   KT     the --kernel-trace --stats pass (KT/ + KT.log holding the bench line), or - for
          a PMC-only summary
@@ -12,6 +12,7 @@ Usage: summarize_profile.py TAG SRC KT [FETCH WRITE] [BOARD] [KERNEL] [SHAPE_JSO
   SHAPE_JSON  the bench's launch_shape that the pinned PMC passes ran (stored as `shape`)
   SQ     a --pmc pass of GRBM_GUI_ACTIVE + SQ_* counters of the same pinned run: the clock
          under load (GRBM_GUI_ACTIVE / 8 XCDs / dispatch duration) and the VALU counts
+  KTPIN  a --kernel-trace pass of the same pinned run: the pinned kernel's average duration
 
 Timed dispatches: bench.py loads each board (k_il_convert), steps the warm-up turns, then
 the timed turns, so the timed launches are the last `launches` stencil dispatches
@@ -58,7 +59,8 @@ def load_rows(path):
     return rows
 
 
-def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=None, sq=None):
+def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=None, sq=None,
+         ktpin=None):
     board = int(board)
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -130,6 +132,14 @@ def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=Non
         if "SQ_ACTIVE_INST_VALU" in med and "SQ_WAVE_CYCLES" in med:
             res["valu_active_per_wave_cycle"] = round(med["SQ_ACTIVE_INST_VALU"] /
                                                       med["SQ_WAVE_CYCLES"], 4)
+    if ktpin and ktpin != "-":
+        rows = load_rows(os.path.join(src, ktpin, "run_kernel_trace.csv"))
+        rows = [r for r in rows if kernel in r["Kernel_Name"]] if kernel else rows
+        # the timed call of tools/kernel_run.py: its last turns / K launches
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[-10:]]
+        res["pinned_trace_launches"] = len(durs)
+        res["pinned_trace_avg_ns"] = statistics.mean(durs) if durs else None
+        res["pinned_trace_kernels"] = sorted({r["Kernel_Name"] for r in rows[-10:]})
     with open(os.path.join(out, f"{tag}_summary.json"), "w") as f:
         json.dump(res, f, indent=1)
     show = {k: v for k, v in res.items() if k != "bench_line"}
