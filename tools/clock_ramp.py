@@ -4,7 +4,11 @@ Pinned 65536^2 shape (no autotune); HIP events around each gol_step on one strea
   A: 40 calls of 20 turns back to back (after 1 s idle)
   B: 20 calls, 50 ms host sleep before each
   C: 20 calls, each after 20 ms of back-to-back turns (busy GPU right up to the call)
-  D: one call of 2000 turns, then 20 calls back to back"""
+  D: one call of 2000 turns, then 20 calls back to back
+  E: 10 times: ~60 synchronised short calls (2..32 turns, the autotune's sequence timing),
+     then one 20-turn call
+  F: as E, then 4 ms of back-to-back turns, then the 20-turn call
+  G: as E, then a synchronised 5-turn call (bench.py's warm-up), then the 20-turn call"""
 import os
 import statistics
 import sys
@@ -43,19 +47,53 @@ def show(tag, xs):
 
 
 time.sleep(1.0)
-show("A back-to-back after 1 s idle", [call() for _ in range(40)])
+
+
+def a_to_d():
+    show("A back-to-back after 1 s idle", [call() for _ in range(40)])
+    xs = []
+    for _ in range(20):
+        time.sleep(0.05)
+        xs.append(call())
+    show("B 50 ms idle before each", xs)
+    xs = []
+    for _ in range(20):
+        e.step(560)                      # ~20 ms of turns, not waited for
+        xs.append(call())
+    show("C busy right up to each call", xs)
+    long = call(2000)
+    show("D long call (per 20 turns)", [long / 100])
+    show("D then back-to-back", [call() for _ in range(20)])
+
+
+if not os.environ.get("ONLY_EF"):
+    a_to_d()
+
+
+def short_calls():
+    for r in range(2, 33, 1):
+        e.step(r)
+        e.sync()
+        e.step(r)
+        e.sync()
+
+
 xs = []
-for _ in range(20):
-    time.sleep(0.05)
+for _ in range(10):
+    short_calls()
     xs.append(call())
-show("B 50 ms idle before each", xs)
+show("E after synchronised short calls", xs)
 xs = []
-for _ in range(20):
-    e.step(560)                      # ~20 ms of turns, not waited for
+for _ in range(10):
+    short_calls()
+    e.step(120)
     xs.append(call())
-show("C busy right up to each call", xs)
-t0 = time.perf_counter()
-long = call(2000)
-show("D long call (per 20 turns)", [long / 100])
-show("D then back-to-back", [call() for _ in range(20)])
+show("F after short calls + 4 ms busy", xs)
+xs = []
+for _ in range(10):
+    short_calls()
+    e.step(5)                        # the bench: 5 warm-up turns, synchronise, time 20
+    e.sync()
+    xs.append(call())
+show("G after short calls + the bench's 5-turn warm-up", xs)
 e.close()
