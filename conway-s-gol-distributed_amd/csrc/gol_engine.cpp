@@ -130,6 +130,13 @@ struct gol_ctx {
     unsigned *pflags = nullptr;
     size_t pflags_n = 0;
     unsigned pepoch = 0;
+    // K1q (k_tile_stream, large torus boards): turns per block (0 = off) and its tile shape;
+    // the item counter (uncached) and its host mirror (the value the next launch starts from)
+    int stream_k = 0;
+    bool stream_forced = false;              // GOL_STREAM (tests): also on a shared device
+    int stream_tw = 0, stream_th = 0, stream_seg = 0;
+    unsigned *pcounter = nullptr;
+    unsigned pcount = 0;
     // device error word (host-mapped pinned memory; golk::kDevErr*): a k_step_wg wait that gave
     // up writes it, every synchronising call checks it
     unsigned *h_err = nullptr, *d_err = nullptr;
@@ -205,6 +212,7 @@ struct TuneKey {
 };
 struct TuneVal {
     int var, tpl, band, tile_w, tile_seg, persist_k;
+    int stream_k, stream_tw, stream_th, stream_seg;
     float us;
     std::vector<Launch> plan;
     std::vector<std::vector<Launch>> seq;
@@ -416,6 +424,14 @@ Launch plan_launch(gol_ctx *c, int64_t room)
         return Launch{(int)std::min<int64_t>(room, cap), golk::kMultiTilePersist, c->band_multi,
                       c->tile_w, c->tile_seg, c->persist_k};
     }
+    if (c->stream_k > 0 && !is_strip(c) && room >= 2 * c->stream_k) {
+        // K1q: blocks of <= stream_k turns in one launch, up to ~8 ms of work per launch (the
+        // control word and readers are served between launches)
+        const double us = c->tuned_us_per_turn > 0.f ? c->tuned_us_per_turn : 1.0;
+        const int64_t cap = std::max<int64_t>(2 * c->stream_k, (int64_t)(8000.0 / us));
+        return Launch{(int)std::min<int64_t>(room, cap), golk::kMultiTileStream, c->stream_th,
+                      c->stream_tw, c->stream_seg, c->stream_k};
+    }
     if (!c->plan.empty()) {
         if (room > kPlanMax)
             return Launch{c->tpl, c->multi_variant, c->band_multi, c->tile_w, c->tile_seg};
@@ -499,38 +515,72 @@ static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
     return hipSuccess;
 }
 
-// K1p: the uncached block buffers (board-sized) and per-tile flags, allocated on first use
-// (the engine's streams drained first), and one launch of `turns` turns on them
-hipError_t persist_launch(gol_ctx *c, golk::StepArgs a, int turns, int K)
+// K1p / K1q: the uncached block buffers (board-sized), per-tile flags and the item counter,
+// allocated on first use (the engine's streams drained first)
+static hipError_t persist_buffers(gol_ctx *c, long long ntiles)
 {
     const size_t words = (size_t)c->buf_rows * c->pitch;
+    if (c->pu[0] && c->pu[1] && (size_t)ntiles <= c->pflags_n && c->pcounter) return hipSuccess;
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return e;
+    for (auto *&u : c->pu)
+        if (!u && (e = hipExtMallocWithFlags((void **)&u, words * 8, hipDeviceMallocUncached)) !=
+                      hipSuccess)
+            return e;
+    if (!c->pcounter) {
+        if ((e = hipExtMallocWithFlags((void **)&c->pcounter, 64, hipDeviceMallocUncached)) !=
+                hipSuccess ||
+            (e = hipMemset(c->pcounter, 0, 64)) != hipSuccess ||
+            (e = hipDeviceSynchronize()) != hipSuccess)
+            return e;
+        c->pcount = 0;
+    }
+    if ((size_t)ntiles > c->pflags_n) {
+        if (c->pflags) (void)hipFree(c->pflags);
+        c->pflags = nullptr;
+        c->pflags_n = 0;
+        if ((e = hipExtMallocWithFlags((void **)&c->pflags, (size_t)ntiles * sizeof(unsigned),
+                                       hipDeviceMallocUncached)) != hipSuccess ||
+            (e = hipMemset(c->pflags, 0, (size_t)ntiles * sizeof(unsigned))) != hipSuccess ||
+            (e = hipDeviceSynchronize()) != hipSuccess)
+            return e;
+        c->pflags_n = (size_t)ntiles;
+        c->pepoch = 0;
+    }
+    return hipSuccess;
+}
+
+// K1p: one launch of `turns` turns in blocks of K on resident tiles
+hipError_t persist_launch(gol_ctx *c, golk::StepArgs a, int turns, int K)
+{
     const long long ntiles = golk::tile_count(c->nw, a.row_hi - a.row_lo, a.band, a.tile_w,
                                               a.tile_seg);
-    if (!c->pu[0] || (size_t)ntiles > c->pflags_n) {
-        hipError_t e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess) return e;
-        for (auto *&u : c->pu)
-            if (!u && (e = hipExtMallocWithFlags((void **)&u, words * 8,
-                                                 hipDeviceMallocUncached)) != hipSuccess)
-                return e;
-        if ((size_t)ntiles > c->pflags_n) {
-            if (c->pflags) (void)hipFree(c->pflags);
-            c->pflags = nullptr;
-            c->pflags_n = 0;
-            if ((e = hipExtMallocWithFlags((void **)&c->pflags, (size_t)ntiles * sizeof(unsigned),
-                                           hipDeviceMallocUncached)) != hipSuccess ||
-                (e = hipMemset(c->pflags, 0, (size_t)ntiles * sizeof(unsigned))) != hipSuccess ||
-                (e = hipDeviceSynchronize()) != hipSuccess)
-                return e;
-            c->pflags_n = (size_t)ntiles;
-            c->pepoch = 0;
-        }
-    }
+    if (hipError_t e = persist_buffers(c, ntiles)) return e;
     // flags of earlier launches are at most their epoch + blocks - 1: start above them all
     const unsigned nblocks = (unsigned)((turns + K - 1) / K);
     const unsigned epoch = c->pepoch + 1;
     c->pepoch = epoch + nblocks;
     return golk::launch_tile_persist(a, turns, K, c->pu[0], c->pu[1], c->pflags, epoch, c->stream);
+}
+
+// K1q: one launch of `turns` turns in blocks of K, (block, tile) items taken from the counter
+hipError_t stream_launch(gol_ctx *c, golk::StepArgs a, int turns, int K)
+{
+    const long long ntiles = golk::tile_count(c->nw, a.row_hi - a.row_lo, a.band, a.tile_w,
+                                              a.tile_seg);
+    if (hipError_t e = persist_buffers(c, ntiles)) return e;
+    const unsigned nblocks = (unsigned)((turns + K - 1) / K);
+    const unsigned epoch = c->pepoch + 1;
+    unsigned grid = 0;
+    // GOL_STREAM_GRID (tests): cap the workgroups, so that each takes many items
+    const int max_grid = getenv("GOL_STREAM_GRID") ? atoi(getenv("GOL_STREAM_GRID")) : 0;
+    const hipError_t e = golk::launch_tile_stream(a, turns, K, c->pu[0], c->pu[1], c->pflags,
+                                                  epoch, c->pcounter, c->pcount, c->ncu, max_grid,
+                                                  &grid, c->stream);
+    if (e != hipSuccess) return e;
+    c->pepoch = epoch + nblocks;
+    c->pcount += (unsigned)(ntiles * nblocks) + grid;   // items + one overshoot per workgroup
+    return hipSuccess;
 }
 
 // ---------------------------------------------------------------- k_step_tile planning
@@ -1182,6 +1232,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     // with the least total measured time (plan_launch).  All candidates run on the
     // interleaved layout, so launches of different kernels mix freely.
     std::vector<Launch> plan;
+    float stream_best = 0.f;
     if (tune_k && tune_variant && pick_t > 0.f) {
         struct Fam {
             int var, K, band, tw, seg;
@@ -1330,6 +1381,60 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             }
         }
         c->seq = std::move(seqs);
+        // K1q for the tile family: 240 turns as one k_tile_stream launch in blocks of Kp
+        // turns (one start and one tail instead of one per launch), against the tuned
+        // steady rate; kept when >= 2 % faster.  Torus engines only (a strip's halo window
+        // shrinks its rows from launch to launch).
+        c->stream_k = 0;
+        if (!is_strip(c) && !getenv("GOL_NO_STREAM")) {
+            const Fam *tf = nullptr;
+            for (const Fam &f : fams)
+                if (f.var == golk::kMultiTile) tf = &f;
+            const int N = 240;
+            float sbest = 0.f;
+            int sk = 0, sband = 0;
+            for (int Kp : {tf ? tf->K : 0, 12, 16, 20, 24, 32}) {
+                if (!tf || Kp < 2 || Kp > golk::kMaxTurnsPerLaunch || tf->band_k[Kp] <= 0 ||
+                    !golk::tile_stream_ok(c->nw, c->buf_rows, Kp, tf->band_k[Kp], tf->tw, tf->seg))
+                    continue;
+                a.band = tf->band_k[Kp];
+                a.multi_variant = golk::kMultiTile;
+                a.tile_w = tf->tw;
+                a.tile_seg = tf->seg;
+                a.in = c->board[0];
+                a.out = c->board[1];
+                float v = 0.f;
+                for (int pass = 0; pass < 3; ++pass) {
+                    float ms = 0.f;
+                    const bool ok = hipEventRecord(e0, c->stream) == hipSuccess &&
+                                    stream_launch(c, a, N, Kp) == hipSuccess &&
+                                    hipEventRecord(e1, c->stream) == hipSuccess &&
+                                    hipEventSynchronize(e1) == hipSuccess &&
+                                    hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+                    if (ok && (v == 0.f || ms / N < v)) v = ms / N;
+                }
+                if (getenv("GOL_AUTOTUNE_LOG"))
+                    fprintf(stderr, "autotune stream %dx%d K=%d band=%d tile=%d,%d us_per_turn=%.3f "
+                            "(tuned %.3f)\n", c->cfg.width, c->buf_rows, Kp, a.band, tf->tw, tf->seg,
+                            v * 1000.f, best * 1000.f);
+                if (v > 0.f && (sbest == 0.f || v < sbest)) {
+                    sbest = v;
+                    sk = Kp;
+                    sband = a.band;
+                }
+            }
+            // (a wait that gave up while timing: no K1q, and the junk board's error word is
+            // cleared -- the board is refilled before use)
+            const bool bad = check_dev_err(c) != GOL_OK;
+            if (bad) clear_dev_err(c);
+            if (sk && sbest < 0.98f * best && !bad) {
+                c->stream_k = sk;
+                c->stream_tw = tf->tw;
+                c->stream_th = sband;
+                c->stream_seg = tf->seg;
+                stream_best = sbest;
+            }
+        }
         if (getenv("GOL_AUTOTUNE_LOG")) {
             for (const Fam &f : fams)
                 for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k)
@@ -1358,7 +1463,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
     for (int &b : c->band_at) b = 0;
     if (plan.empty()) c->seq.clear();
     c->plan = std::move(plan);
-    c->tuned_us_per_turn = best * 1000.f;
+    c->tuned_us_per_turn = (stream_best > 0.f ? stream_best : best) * 1000.f;
 }
 
 }  // namespace
@@ -1553,6 +1658,20 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
                 c->persist_forced = true;
             }
         }
+        if (const char *v = getenv("GOL_STREAM")) {        // tests / experiments: K1q blocks
+            const int sk = atoi(v);
+            if (sk > 0) {
+                if (c->multi_variant != golk::kMultiTile || is_strip(c) ||
+                    !golk::tile_stream_ok(c->nw, c->buf_rows, sk, c->band_multi, c->tile_w,
+                                          c->tile_seg))
+                    return bail(GOL_EINVAL);
+                c->stream_k = sk;
+                c->stream_forced = true;
+                c->stream_tw = c->tile_w;
+                c->stream_th = c->band_multi;
+                c->stream_seg = c->tile_seg;
+            }
+        }
     }
     const char *at = getenv("GOL_AUTOTUNE");
     const bool tuning = !(cfg->flags & GOL_FLAG_NO_AUTOTUNE) && (!at || atoi(at) != 0) &&
@@ -1580,6 +1699,10 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
             c->tile_w = v.tile_w;
             c->tile_seg = v.tile_seg;
             c->persist_k = v.persist_k;
+            c->stream_k = v.stream_k;
+            c->stream_tw = v.stream_tw;
+            c->stream_th = v.stream_th;
+            c->stream_seg = v.stream_seg;
             c->plan = v.plan;
             c->seq = v.seq;
             c->tuned_us_per_turn = v.us;
@@ -1596,7 +1719,8 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         if (use_cache) {
             std::lock_guard<std::mutex> lk(g_tune_mu);
             g_tune[key] = TuneVal{c->multi_variant, c->tpl, c->band_multi, c->tile_w,
-                                  c->tile_seg, c->persist_k, c->tuned_us_per_turn, c->plan,
+                                  c->tile_seg, c->persist_k, c->stream_k, c->stream_tw,
+                                  c->stream_th, c->stream_seg, c->tuned_us_per_turn, c->plan,
                                   c->seq};
         }
     }
@@ -1628,6 +1752,7 @@ void gol_destroy(gol_ctx *c)
         if (c->pg_flags) (void)hipFree(c->pg_flags);
         for (auto *u : c->pu)
             if (u) (void)hipFree(u);
+        if (c->pcounter) (void)hipFree(c->pcounter);
         if (c->pflags) (void)hipFree(c->pflags);
         if (c->blocked) (void)hipFree(c->blocked);
         if (c->counts) (void)hipFree(c->counts);
@@ -1966,7 +2091,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
             a.counts = nullptr;
             a.band = plan.band;
             a.multi_variant = plan.var;
-            if (plan.var == golk::kMultiTile || plan.var == golk::kMultiTilePersist) {
+            if (plan.var == golk::kMultiTile || plan.var == golk::kMultiTilePersist ||
+                plan.var == golk::kMultiTileStream) {
                 a.tile_w = plan.tw;
                 a.tile_seg = plan.seg;
             }
@@ -1977,6 +2103,8 @@ int step_impl(gol_ctx *c, int64_t turns, hipStream_t xstream,
 #endif
             if (plan.var == golk::kMultiTilePersist) {
                 HIP_OR_FAIL(c, persist_launch(c, a, k, plan.blk));
+            } else if (plan.var == golk::kMultiTileStream) {
+                HIP_OR_FAIL(c, stream_launch(c, a, k, plan.blk));
             } else if (split && in_lo < in_hi) {
                 golk::StepArgs b = a;
                 // concurrent launches cannot share the published-row scratch
@@ -2105,9 +2233,9 @@ int gol_last_launch_tiles(gol_ctx *c, int32_t *tile_w, int32_t *tile_seg, int32_
     const int n = (int)std::min<size_t>((size_t)cap, c->last.size());
     for (int i = 0; i < n; ++i) {
         const Launch &L = c->last[i];
-        const bool p = L.var == golk::kMultiTilePersist;
+        const bool p = L.var == golk::kMultiTilePersist || L.var == golk::kMultiTileStream;
         const bool t = L.k > 1 && (L.var == golk::kMultiTile || p);
-        const int depth = p ? L.blk : L.k;               // (K1p: the waves fit one block)
+        const int depth = p ? L.blk : L.k;               // (K1p / K1q: the waves fit one block)
         tile_w[i] = t ? L.tw : 0;
         tile_seg[i] = t ? L.seg : 0;
         waves[i] = t ? golk::tile_waves(depth, L.band, L.tw, L.seg) : 0;
@@ -2129,6 +2257,14 @@ int gol_tile_persist_codes(int32_t *codes, int32_t cap)
     const int n = (int)std::size(golk::kTilePersistCodes);
     if (cap < 0 || (cap > 0 && !codes)) return GOL_EINVAL;
     for (int i = 0; i < std::min(n, (int)cap); ++i) codes[i] = golk::kTilePersistCodes[i];
+    return n;
+}
+
+int gol_tile_stream_codes(int32_t *codes, int32_t cap)
+{
+    const int n = (int)std::size(golk::kTileStreamCodes);
+    if (cap < 0 || (cap > 0 && !codes)) return GOL_EINVAL;
+    for (int i = 0; i < std::min(n, (int)cap); ++i) codes[i] = golk::kTileStreamCodes[i];
     return n;
 }
 

@@ -77,6 +77,8 @@ enum : int {
     kMultiCount = 16,
     kMultiTilePersist = 16, // K1p k_tile_persist: k_step_tile's tiles resident across blocks of
                             //   K turns (engine-internal: small torus boards, never requested)
+    kMultiTileStream = 17,  // K1q k_tile_stream: blocks of K turns over (block, tile) items taken
+                            //   in order by resident workgroups (engine-internal, large boards)
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
 
@@ -207,6 +209,9 @@ constexpr int kTilePersistCodes[] = {102, 103, 104, 106, 108, 112, 116,
                                      403, 404, 406, 408, 412, 416,
                                      2, 3, 4, 6, 8,
                                      503, 504, 506, 508};
+// the codes k_tile_stream (K1q) is instantiated for (gol_tile.hip stream_fn; each pinned by
+// tests/test_gpu_engine.py::test_tile_stream_pinned through gol_tile_stream_codes)
+constexpr int kTileStreamCodes[] = {106, 506, 512, 524};
 constexpr bool tile_code_shipped(int code)
 {
     for (int c : kTileCodes)
@@ -226,6 +231,14 @@ hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s);
 bool tile_persist_ok(int nw, int rows, int turns, int K, int tile_h, int tile_w, int seg, int ncu);
 hipError_t launch_tile_persist(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
                                unsigned *flags, unsigned epoch, hipStream_t s);
+// K1q k_tile_stream (gol_tile.h): `turns` turns in blocks of K over (block, tile) items taken
+// from *counter (value `base` at the launch) by min(items, CUs x occupancy, max_grid if > 0)
+// workgroups, whose count goes to *grid (the counter advances by items + grid).  Same u0 / u1 / flags contract
+// as K1p; tile_stream_ok: an instantiated code and K within the tile rows (no residency need).
+bool tile_stream_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg);
+hipError_t launch_tile_stream(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
+                              unsigned *flags, unsigned epoch, unsigned *counter, unsigned base,
+                              int ncu, int max_grid, unsigned *grid, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);
 

@@ -62,9 +62,11 @@ constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 // shifts + 4W v_bitop3 instead of W x (2 + 2 + 4) -- 48 instead of 52 SIMD cycles per 4096
 // cell-updates with the rule.
 // One pass of K turns over one tile (the body of k_step_tile, and of each block of
-// k_tile_persist).  PERSIST: the workgroup stays for further passes, so a wave that leaves the
-// trapezoid does not end -- it skips its remaining turns (ORD 1/2: it still meets every
-// workgroup barrier of them) and the pass returns to the caller on every path.
+// k_tile_persist / item of k_tile_stream).  PERSIST: the workgroup stays for further passes,
+// so no wave leaves the trapezoid early -- every wave runs every turn (a wave past the
+// trapezoid computes halo rows nobody reads) and the pass returns on every path.  (A leaving
+// wave would have to meet the barriers of its remaining turns, and that exit path alone took
+// the SEG 24 pass from 80 to 126 VGPRs.)
 template <int SEG, int ORD, int W, bool PERSIST>
 __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
                                           uint64_t *__restrict__ out, const StepArgs &a,
@@ -383,20 +385,17 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     };
     const int lastrow = 2 * K + TH - 1;
     // a wave leaving the trapezoid at turn t: its rows are all < K or >= K + TH, so it has
-    // nothing to store.  Alone it ends (the barrier stops counting it); in a persistent pass
-    // it meets the K - t barriers its turns would have met (ORD 4: none -- its flag says it
-    // has gone) and falls through to the (empty) store
+    // nothing to store.  It ends (the barrier stops counting it; ORD 4: its flag says it has
+    // gone).  Persistent passes keep every wave to the end of the pass.
     auto leave = [&](int t) {
         if constexpr (ORD == 4) {
             if (lane == 0) flag[wave] = 0x7fffffff;
-        } else if constexpr (PERSIST && ORD != 3) {
-            for (; t < K; ++t) __syncthreads();
         }
     };
     bool gone = false;
     if constexpr (!kPairs) {
         for (int t = 0; t < K; ++t) {
-            if (wrow1 <= t || wrow0 > lastrow - t) {           // (wave-uniform)
+            if (!PERSIST && (wrow1 <= t || wrow0 > lastrow - t)) {   // (wave-uniform)
                 leave(t);
                 gone = true;
                 break;
@@ -405,14 +404,14 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         }
     } else {
         for (int t = 0; t < K; t += 2) {
-            if (wrow1 <= t || wrow0 > lastrow - t) {
+            if (!PERSIST && (wrow1 <= t || wrow0 > lastrow - t)) {
                 leave(t);
                 gone = true;
                 break;
             }
             turn(std::integral_constant<int, 0>{}, 0, t);
             if (t + 1 == K) break;
-            if (wrow1 <= t + 1 || wrow0 > lastrow - t - 1) {
+            if (!PERSIST && (wrow1 <= t + 1 || wrow0 > lastrow - t - 1)) {
                 leave(t + 1);
                 gone = true;
                 break;
@@ -514,6 +513,92 @@ __global__ __launch_bounds__(1024, 1) void k_tile_persist(
         if (threadIdx.x == 0)
             __hip_atomic_store(flags + tile, epoch + (unsigned)b + 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (gave_up && a.err)
+        __hip_atomic_store(a.err, kDevErrTileFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+
+// K1q k_tile_stream: K1p's blocks for boards whose tiles do not all fit at once.  One launch
+// runs `turns` turns as blocks of <= K turns; the (block, tile) items are taken in order from
+// a device counter by a grid of resident workgroups, so one launch has one start and one tail
+// instead of one per K turns (a K1t launch costs ~55 us besides its turns at 65536^2).  Item
+// i = b * ntiles + j is tile row (j / ntx + 2 b) mod nty, column j % ntx of block b: every
+// item of block b is taken before any of block b + 1, and an item waits only for its 8
+// neighbours' block b - 1 (flags as K1p: epoch + b once a tile's block-b stores completed),
+// which were taken earlier and so are running or done -- no deadlock whatever the residency.
+// Rotating the tile rows by 2 per block puts the first items of a block on rows whose
+// neighbours were among the first of the block before (the torus wrap would otherwise make
+// the first row wait for the previous block's last).  Block b reads u[(b-1) % 2] (block 0:
+// `in`) and writes u[b % 2] (the last block: `out`), as K1p.  counter counts across
+// launches: each workgroup takes one item past the end before it leaves, so a launch
+// advances it by items + grid; `base` is its value at the launch (unsigned wrap).
+// (the item loop holds registers across items: bound them to k_step_tile's budget -- 80
+// VGPRs at SEG 24, 6 waves per SIMD; 64 below, 8)
+template <int SEG, int ORD, int W>
+__global__ __launch_bounds__(1024, (SEG >= 20 ? 6 : 8)) void k_tile_stream(
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t *u0, uint64_t *u1,
+    StepArgs a, int turns, int K, int ntx, int ntiles, unsigned *flags, unsigned epoch,
+    unsigned *counter, unsigned base)
+{
+    __shared__ unsigned next_item;
+    const int nty = ntiles / ntx;
+    const int nblocks = (turns + K - 1) / K, kbase = turns / nblocks, extra = turns % nblocks;
+    const unsigned nitems = (unsigned)nblocks * (unsigned)ntiles;
+    bool gave_up = false;
+    if (threadIdx.x == 0)
+        next_item = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base;
+    __syncthreads();
+    for (;;) {
+        const unsigned item = next_item;
+        __syncthreads();                                  // (everyone has read next_item)
+        if (item >= nitems) break;                        // (workgroup-uniform)
+        // the next item's fetch overlaps this one (its latency is a memory round trip, in
+        // flight with the tile loads); thread 0 hands it over at the end of the item
+        unsigned nxt = 0;
+        if (threadIdx.x == 0)
+            nxt = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - base;
+        const int b = (int)(item / (unsigned)ntiles), j = (int)(item % (unsigned)ntiles);
+        const int ty = (j / ntx + 2 * b) % nty, tx = j % ntx;
+        const int tile = ty * ntx + tx;
+        const int k = kbase + (b < extra ? 1 : 0);
+        if (b > 0) {
+            if (threadIdx.x < 8) {                        // one neighbour per lane 0..7
+                const int jj = (int)threadIdx.x + (threadIdx.x >= 4 ? 1 : 0);   // skip (0, 0)
+                const int dy = jj / 3 - 1, dx = jj % 3 - 1;
+                const int ny = (ty + dy + nty) % nty, nx = (tx + dx + ntx) % ntx;
+                const unsigned want = epoch + (unsigned)b;
+                unsigned *f = flags + ny * ntx + nx;
+                bool seen = false;
+                for (int spin = 0; !seen && spin < GOL_TILE_SPIN_LIMIT; ++spin) {
+                    const unsigned v =
+                        __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    seen = (int)(v - want) >= 0;
+                    if (!seen) __builtin_amdgcn_s_sleep(2);
+                }
+                gave_up |= !seen;
+            }
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __syncthreads();
+        }
+        const uint64_t *src = b == 0 ? in : ((b & 1) ? u0 : u1);
+        uint64_t *dst = b + 1 == nblocks ? out : ((b & 1) ? u1 : u0);
+        // (the shape's scalars pass through an empty asm every item, so the lane constants
+        // tile_pass derives from them are recomputed per item rather than hoisted out of the
+        // loop and held in VGPRs across it: that spilled at SEG 24)
+        StepArgs aa = a;
+        asm volatile("" : "+s"(aa.tile_w), "+s"(aa.band), "+s"(aa.nw), "+s"(aa.pitch),
+                     "+s"(aa.modrows));
+        tile_pass<SEG, ORD, W, true>(src, dst, aa, k, tile, ntx);
+        if (b + 1 < nblocks) {
+            __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // this wave's stores are done
+            __syncthreads();                                     // ... and every wave's
+            if (threadIdx.x == 0)
+                __hip_atomic_store(flags + tile, epoch + (unsigned)b + 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (threadIdx.x == 0) next_item = nxt;
+        __syncthreads();                                  // (and the LDS slots are free again)
     }
     if (gave_up && a.err)
         __hip_atomic_store(a.err, kDevErrTileFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

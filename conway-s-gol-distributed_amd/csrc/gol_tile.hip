@@ -1,6 +1,7 @@
 // gol_tile.hip -- the k_step_tile instantiation table (K1t, gol_tile.h) and its launcher.
 #include "gol_tile.h"
 
+#include <algorithm>
 #include <iterator>
 #include <map>
 #include <mutex>
@@ -70,6 +71,19 @@ static void *tile_fn6(int seg)
     case 12: return reinterpret_cast<void *>(&k_step_tile<12, 6, 1>);
     case 16: return reinterpret_cast<void *>(&k_step_tile<16, 6, 1>);
     case 24: return reinterpret_cast<void *>(&k_step_tile<24, 6, 1>);
+    default: return nullptr;
+    }
+}
+
+// k_tile_stream instantiations (K1q, large boards): the 65536^2 and 16384^2 shape families
+static void *stream_fn(int code)
+{
+    static_assert(std::size(kTileStreamCodes) == 4, "stream_fn covers kTileStreamCodes");
+    switch (code) {
+    case 106: return reinterpret_cast<void *>(&k_tile_stream<6, 1, 1>);
+    case 506: return reinterpret_cast<void *>(&k_tile_stream<6, 5, 1>);
+    case 512: return reinterpret_cast<void *>(&k_tile_stream<12, 5, 1>);
+    case 524: return reinterpret_cast<void *>(&k_tile_stream<24, 5, 1>);
     default: return nullptr;
     }
 }
@@ -195,6 +209,50 @@ hipError_t launch_tile_persist(const StepArgs &a, int turns, int K, uint64_t *u0
     int t = turns, k = K, ntx_arg = ntx, nt = (int)ntiles;
     void *params[] = {&in, &out, &u0, &u1, &args, &t, &k, &ntx_arg, &nt, &flags, &epoch};
     return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params, tile_lds_bytes(threads, 1), s);
+}
+
+}  // namespace golk
+
+namespace golk {
+
+bool tile_stream_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg)
+{
+    if (!stream_fn(seg) || !tile_shape_ok(nw, K, tile_h, tile_w, seg)) return false;
+    const int nty = (rows + tile_h - 1) / tile_h;
+    const int last_h = rows - (nty - 1) * tile_h;
+    return K <= tile_h && K <= last_h;   // a tile's K halo rows come from adjacent tile rows only
+}
+
+hipError_t launch_tile_stream(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
+                              unsigned *flags, unsigned epoch, unsigned *counter, unsigned base,
+                              int ncu, int max_grid, unsigned *grid_out, hipStream_t s)
+{
+    const int rows = a.row_hi - a.row_lo;
+    void *fn = stream_fn(a.tile_seg);
+    if (!fn || !tile_stream_ok(a.nw, rows, K, a.band, a.tile_w, a.tile_seg) || turns < 1 || ncu < 1)
+        return hipErrorInvalidValue;
+    const int ntx = (a.nw + a.tile_w - 1) / a.tile_w;
+    const long long ntiles = (long long)ntx * ((rows + a.band - 1) / a.band);
+    const long long nitems = ntiles * ((turns + K - 1) / K);
+    if (ntiles <= 0 || nitems > (1ll << 30)) return hipErrorInvalidValue;
+    const int threads = 64 * tile_waves(K, a.band, a.tile_w, a.tile_seg);
+    const size_t lds = tile_lds_bytes(threads, 1);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess ||
+        per_cu < 1)
+        return hipErrorInvalidValue;
+    long long g = std::min<long long>(nitems, (long long)ncu * per_cu);
+    if (max_grid > 0) g = std::min<long long>(g, max_grid);   // (tests: few workgroups)
+    const unsigned grid = (unsigned)g;
+    StepArgs args = a;
+    const uint64_t *in = a.in;
+    uint64_t *out = a.out;
+    int t = turns, k = K, ntx_arg = ntx, nt = (int)ntiles;
+    void *params[] = {&in, &out, &u0, &u1, &args, &t, &k, &ntx_arg, &nt, &flags, &epoch, &counter,
+                      &base};
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(threads), params, lds, s);
+    if (e == hipSuccess && grid_out) *grid_out = grid;
+    return e;
 }
 
 }  // namespace golk

@@ -125,6 +125,7 @@ SIGNATURES = {
                                      ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     "gol_tile_codes": (_i32, [ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     "gol_tile_persist_codes": (_i32, [ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
+    "gol_tile_stream_codes": (_i32, [ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     "gol_stream_wait": (_i32, [_vp, _vp]),
     "gol_step_overlap": (_i32, [_vp, _i64, _vp]),
     "gol_snapshot": (_i32, [_vp, _i64p, _i64p]),

@@ -177,6 +177,9 @@ int gol_tile_codes(int32_t *codes, int32_t cap);
 /* The subset of those the persistent tile kernel (K1p: small torus boards, tiles resident
  * across blocks of turns) runs; same convention. */
 int gol_tile_persist_codes(int32_t *codes, int32_t cap);
+/* The subset the streamed tile kernel (K1q: large torus boards, blocks of turns over
+ * (block, tile) items taken in order by resident workgroups) runs; same convention. */
+int gol_tile_stream_codes(int32_t *codes, int32_t cap);
 /* Lock-free progress read for a controlling thread: *turn = turns enqueued so far (the
  * board reaches it at the next gol_sync), *parked = 1 while gol_step is parked on PAUSE
  * (the board is then complete at *turn).  Either pointer may be NULL. */

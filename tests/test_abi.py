@@ -81,6 +81,11 @@ def test_tile_codes_are_the_pinned_list():
     buf = (C.c_int32 * n)()
     assert L.gol_tile_persist_codes(buf, n) == n
     assert tuple(buf) == TILE_PERSIST_CODES and set(buf) <= set(TILE_CODES)
+    from conftest import TILE_STREAM_CODES
+    n = L.gol_tile_stream_codes(None, 0)
+    buf = (C.c_int32 * n)()
+    assert L.gol_tile_stream_codes(buf, n) == n
+    assert tuple(buf) == TILE_STREAM_CODES and set(buf) <= set(TILE_CODES)
 
 
 def test_lib_is_gfx950_code_object():

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import golden_data as G
-from conftest import TILE_CODES, TILE_PERSIST_CODES, tools_only
+from conftest import TILE_CODES, TILE_PERSIST_CODES, TILE_STREAM_CODES, tools_only
 
 pytestmark = pytest.mark.gpu
 
@@ -757,6 +757,49 @@ def test_tile_persist_pinned(gol, oracle, monkeypatch, code, shape):
         e.step(turns)
         plan = e.last_launches()
         assert [v for _, v, _ in plan] == [16] and plan[0][0] == turns, plan
+        t = e.last_launch_tiles(blocks=True)[0]
+        assert (t[0], t[1], t[3]) == (tw, code, K), t
+        mid = e.read_packed()
+        e.step(turns + 3)
+        got = e.read_packed()
+    want = oracle.bit_run(start, w, turns)
+    assert np.array_equal(mid, want)
+    assert np.array_equal(got, oracle.bit_run(want, w, turns + 3))
+
+
+STREAM_SHAPES = [
+    # (width, height, tile_w, tile_h, K, turns, workgroups): items taken by 3 workgroups (each
+    # takes many, in order, waiting on earlier ones), a single tile row / column, and a board
+    # with more items than resident workgroups
+    (4224, 157, 14, 100, 8, 43, 3),
+    (4224, 157, 30, 60, 12, 40, 5),
+    (1024, 64, 14, 64, 8, 35, 2),     # one tile row: the up and down neighbours are itself
+    (896, 90, 14, 30, 10, 31, 0),     # one tile column (14 words), 3 tile rows
+    (8192, 2048, 30, 128, 20, 62, 0),
+]
+
+
+@pytest.mark.parametrize("code", TILE_STREAM_CODES)
+@pytest.mark.parametrize("shape", range(len(STREAM_SHAPES)))
+def test_tile_stream_pinned(gol, oracle, monkeypatch, code, shape):
+    """K1q k_tile_stream (blocks of K turns over (block, tile) items taken in order from a
+    device counter; borders through uncached memory and per-tile flags, as K1p) for every
+    instantiation it has, against the oracle: one launch runs all the turns, a second call
+    continues from the first's board (the counter and the flags' epoch carry over)."""
+    w, h, tw, th, K, turns, grid = STREAM_SHAPES[shape]
+    if code % 100 * (64 // (tw + 2)) * 16 < th + 2 * K:
+        pytest.skip("tile taller than 16 waves of this segment")
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+    monkeypatch.setenv("GOL_TILE", f"{tw},{code}")
+    monkeypatch.setenv("GOL_STREAM", str(K))
+    if grid:
+        monkeypatch.setenv("GOL_STREAM_GRID", str(grid))
+    start = oracle.gen_random(code * 5 + shape, w, h)
+    with _engine(gol, w, h, band_rows=th, turns_per_launch=K) as e:
+        e.load_packed(start)
+        e.step(turns)
+        plan = e.last_launches()
+        assert [v for _, v, _ in plan] == [17] and plan[0][0] == turns, plan
         t = e.last_launch_tiles(blocks=True)[0]
         assert (t[0], t[1], t[3]) == (tw, code, K), t
         mid = e.read_packed()
