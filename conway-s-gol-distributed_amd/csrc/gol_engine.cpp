@@ -1394,10 +1394,14 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             float sbest = 0.f;
             int sk = 0, sband = 0;
             for (int Kp : {tf ? tf->K : 0, 12, 16, 20, 24, 32}) {
-                if (!tf || Kp < 2 || Kp > golk::kMaxTurnsPerLaunch || tf->band_k[Kp] <= 0 ||
-                    !golk::tile_stream_ok(c->nw, c->buf_rows, Kp, tf->band_k[Kp], tf->tw, tf->seg))
+                if (!tf || Kp < 2 || Kp > golk::kMaxTurnsPerLaunch || tf->band_k[Kp] <= 0)
                     continue;
-                a.band = tf->band_k[Kp];
+                // equal tile rows (the same count): a last tile row shorter than K would take
+                // its halo from two tile rows up
+                const int nty = (c->buf_rows + tf->band_k[Kp] - 1) / tf->band_k[Kp];
+                const int th = (c->buf_rows + nty - 1) / nty;
+                if (!golk::tile_stream_ok(c->nw, c->buf_rows, Kp, th, tf->tw, tf->seg)) continue;
+                a.band = th;
                 a.multi_variant = golk::kMultiTile;
                 a.tile_w = tf->tw;
                 a.tile_seg = tf->seg;

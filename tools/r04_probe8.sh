@@ -9,10 +9,10 @@ step() { local name=$1 t=$2; shift 2
   echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log" | cut -c1-300
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc; }
 step stream_parity 300 python -u -m pytest tests/test_gpu_engine.py -q -x --timeout 150 --timeout-method thread -k "tile_stream_pinned"
-S65=30:336:524:20,14:720:524:24,30:536:524:20,30:344:524:12,14:744:524:12
+S65=30:335:524:20,14:713:524:24,30:536:524:20,30:344:524:12,14:744:524:12
 step sweep65_plain 300 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes $S65
-step sweep65_s20 300 env GOL_STREAM=20 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 30:336:524:20,30:536:524:20
-step sweep65_s24 300 env GOL_STREAM=24 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 14:720:524:24
+step sweep65_s20 300 env GOL_STREAM=20 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 30:335:524:20,30:536:524:20
+step sweep65_s24 300 env GOL_STREAM=24 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 14:713:524:24
 step sweep65_s12 300 env GOL_STREAM=12 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 30:344:524:12,14:744:524:12
 step sweep16_s 300 env GOL_STREAM=32 python -u tools/tile_sweep.py --size 16384 --turns 640 --rounds 3 --shapes 14:316:106:32
 step auto65 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --auto
