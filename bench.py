@@ -249,6 +249,8 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
 
 
 KERNELS = {16: "k_tile_persist<K> (k_step_tile's 2-D tiles resident across blocks of turns)",
+           17: "k_tile_stream<K> (k_step_tile's 2-D tiles in blocks of turns, items taken in "
+               "order by resident workgroups: one launch start and tail per step)",
            7: "k_step_skew<K> (interleaved layout, one pipeline per wave)",
            8: "k_step_wg<K> (pipeline split over a workgroup, band tiles)",
            9: "k_step_wg<K> (pipeline split over a workgroup, helix tiles)",
@@ -272,9 +274,9 @@ def launch_shape(plan, tiles, kvar, kdepth):
     for (k, v, band), t in zip(plan, tiles or [(0, 0, 0, 0)] * len(plan)):
         if v == kvar and k == kdepth:
             sh = {"kernel": v, "turns": k, "band_rows": band}
-            if v in (15, 16) and t[0] > 0:
+            if v in (15, 16, 17) and t[0] > 0:
                 tw, code, waves, blk = t
-                if v == 16:
+                if v in (16, 17):
                     sh["block_turns"] = blk
                 words = code // 1000 + 1
                 sh["tile"] = {"code": code, "width_words": tw * words, "width_lanes": tw,

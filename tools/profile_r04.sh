@@ -46,8 +46,11 @@ for i, alt in enumerate(x for x in os.environ.get("ALT_HEADLINE", "").split(",")
         boards.append((f"h{i + 2}", boards[0][1], sh))
 for name, size, sh in boards:
     k = sh["turns"]
-    args = f"--size {size} --mv {15 if sh['kernel'] in (15, 16) else sh['kernel']} --band {sh['band_rows']}"
-    if sh["kernel"] == 16:
+    args = f"--size {size} --mv {15 if sh['kernel'] in (15, 16, 17) else sh['kernel']} --band {sh['band_rows']}"
+    if sh["kernel"] == 17:
+        t = sh["tile"]
+        args += f" --tile {t['width_lanes']},{t['code']} --tpl {sh['block_turns']} --stream {sh['block_turns']}"
+    elif sh["kernel"] == 16:
         t = sh["tile"]
         args += f" --tile {t['width_lanes']},{t['code']} --tpl {sh['block_turns']} --persist {sh['block_turns']}"
     elif sh["kernel"] == 15:
@@ -58,6 +61,8 @@ for name, size, sh in boards:
     turns = k * (10 if size >= 65536 else 40)
     if sh.get("kernel") == 16:
         turns = 4 * k
+    if sh.get("kernel") == 17:
+        turns = k            # (one launch of the bench's size per step)
     print(name, size, k, json.dumps(sh, separators=(",", ":")), args, "--turns", turns)
 PY
 cat "$O/pins.txt"

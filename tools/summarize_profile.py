@@ -48,7 +48,8 @@ def board_segments(rows):
             segs.append(cur)
         elif "k_fill_random" in name:
             cur = None
-        elif cur is not None and ("k_step" in name or "k_tile_persist" in name):
+        elif cur is not None and ("k_step" in name or "k_tile_persist" in name or
+                                  "k_tile_stream" in name):
             cur.append(r)
     return segs
 

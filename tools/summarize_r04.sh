@@ -8,7 +8,7 @@ O="$R/gpurun_out/prof4"
 board_of() { case $1 in h) echo 0;; c3) echo 1;; c2) echo 2;; *) echo -;; esac; }
 while read -r name size k shape args; do
   kid=$(python3 -c "import json,sys; print(json.loads(sys.argv[1])['kernel'])" "$shape")
-  case $kid in 15) kn=k_step_tile;; 16) kn=k_tile_persist;; 7) kn=k_step_skew;; *) kn=k_step_wg;; esac
+  case $kid in 15) kn=k_step_tile;; 16) kn=k_tile_persist;; 17) kn=k_tile_stream;; 7) kn=k_step_skew;; *) kn=k_step_wg;; esac
   b=$(board_of "$name")
   kt=kt; [ "$b" = - ] && { kt=-; b=0; }
   python3 "$R/tools/summarize_profile.py" "r04_k${k}_${size}_${name}" "$O" "$kt" \
