@@ -1277,110 +1277,6 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                         plan[r] = Launch{k, f.var, f.band_k[k], f.tw, f.seg};
                     }
                 }
-        // Short steps (r <= kSeqMax turns, e.g. the bench's 20-turn call): the DP adds
-        // back-to-back launch times, but a gol_step of r turns starts from a synchronised
-        // stream, and two plans within a few % of each other by the sum traded places as the
-        // bench's single timed call (65536^2 x 20: 2 x k_step_skew K = 10 vs 1 x k_step_tile
-        // K = 20, profiles/r03b_plan_choice.log).  So for every r the DP's plan, the best plan
-        // of each family alone and each family's single launch of depth r are timed as whole
-        // sequences the way gol_step runs them -- host wall time from a synchronised stream
-        // to the last launch's completion, best of 5, candidates interleaved -- and the
-        // fastest is kept in seq[r].
-        std::vector<std::vector<Launch>> seqs(kSeqMax + 1);
-        {
-            auto chain = [&](const std::vector<Launch> &pl, int r) {
-                std::vector<Launch> out;
-                for (int q = r; q >= 2 && pl[q].k >= 2; q -= pl[q].k) out.push_back(pl[q]);
-                int n = 0;
-                for (const Launch &L : out) n += L.k;
-                if (n != r) out.clear();
-                return out;
-            };
-            std::vector<std::vector<Launch>> fam_plan;
-            for (const Fam &f : fams) {
-                std::vector<float> cf(kSeqMax + 1, inf);
-                std::vector<Launch> pf(kSeqMax + 1, Launch{});
-                cf[0] = 0.f;
-                for (int r = 2; r <= kSeqMax; ++r)
-                    for (int k = 2; k <= std::min(r, golk::kMaxTurnsPerLaunch); ++k) {
-                        if (f.T[k] <= 0.f || r - k == 1 || cf[r - k] >= inf) continue;
-                        if (cf[r - k] + f.T[k] < cf[r]) {
-                            cf[r] = cf[r - k] + f.T[k];
-                            pf[r] = Launch{k, f.var, f.band_k[k], f.tw, f.seg};
-                        }
-                    }
-                fam_plan.push_back(std::move(pf));
-            }
-            auto same = [](const std::vector<Launch> &x, const std::vector<Launch> &y) {
-                if (x.size() != y.size()) return false;
-                for (size_t i = 0; i < x.size(); ++i)
-                    if (x[i].k != y[i].k || x[i].var != y[i].var || x[i].band != y[i].band ||
-                        x[i].tw != y[i].tw || x[i].seg != y[i].seg)
-                        return false;
-                return true;
-            };
-            auto time_seq = [&](const std::vector<Launch> &sq) -> float {
-                if (hipStreamSynchronize(c->stream) != hipSuccess) return 0.f;
-                const auto t0 = std::chrono::steady_clock::now();
-                bool ok = true;
-                int rep = 0;
-                for (const Launch &L : sq) {
-                    a.band = L.band;
-                    a.multi_variant = L.var;
-                    a.tile_w = L.tw;
-                    a.tile_seg = L.seg;
-                    a.in = c->board[rep & 1];
-                    a.out = c->board[(rep + 1) & 1];
-                    ++rep;
-                    ok = ok && pg_prepare(c, a, L.k) == hipSuccess &&
-                         golk::launch_step_multi(a, L.k, c->stream) == hipSuccess;
-                }
-                ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
-                const std::chrono::duration<float, std::micro> d =
-                    std::chrono::steady_clock::now() - t0;
-                return ok ? d.count() : 0.f;
-            };
-            for (int r = 2; r <= kSeqMax; ++r) {
-                std::vector<std::vector<Launch>> cands;
-                auto add = [&](std::vector<Launch> sq) {
-                    if (sq.empty()) return;
-                    for (const auto &x : cands)
-                        if (same(x, sq)) return;
-                    cands.push_back(std::move(sq));
-                };
-                add(chain(plan, r));
-                for (size_t fi = 0; fi < fams.size(); ++fi) {
-                    add(chain(fam_plan[fi], r));
-                    if (r <= golk::kMaxTurnsPerLaunch && fams[fi].T[r] > 0.f)
-                        add({Launch{r, fams[fi].var, fams[fi].band_k[r], fams[fi].tw,
-                                    fams[fi].seg}});
-                }
-                if (cands.size() <= 1) {
-                    if (!cands.empty()) seqs[r] = cands[0];
-                    continue;
-                }
-                std::vector<float> tt(cands.size(), 0.f);
-                for (int pass = 0; pass < 5; ++pass)
-                    for (size_t i = 0; i < cands.size(); ++i) {
-                        const float v = time_seq(cands[i]);
-                        if (v > 0.f && (tt[i] == 0.f || v < tt[i])) tt[i] = v;
-                    }
-                size_t bi = 0;
-                for (size_t i = 1; i < cands.size(); ++i)
-                    if (tt[i] > 0.f && (tt[bi] == 0.f || tt[i] < tt[bi])) bi = i;
-                if (tt[bi] > 0.f) seqs[r] = cands[bi];
-                if (getenv("GOL_AUTOTUNE_LOG") && (r == 8 || r == 16 || r == 20 || r == 32))
-                    for (size_t i = 0; i < cands.size(); ++i) {
-                        fprintf(stderr, "autotune seq %d turns%s %.1f us =", r,
-                                i == bi ? " (pick)" : "", tt[i]);
-                        for (const Launch &L : cands[i])
-                            fprintf(stderr, " %d(var %d, band %d, tile %d,%d)", L.k, L.var,
-                                    L.band, L.tw, L.seg);
-                        fprintf(stderr, "\n");
-                    }
-            }
-        }
-        c->seq = std::move(seqs);
         // K1q for the tile family: 240 turns as one k_tile_stream launch in blocks of Kp
         // turns (one start and one tail instead of one per launch), against the tuned
         // steady rate; kept when >= 2 % faster.  Torus engines only (a strip's halo window
@@ -1439,6 +1335,123 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
                 stream_best = sbest;
             }
         }
+        // Short steps (r <= kSeqMax turns, e.g. the bench's 20-turn call): the DP adds
+        // back-to-back launch times, but a gol_step of r turns starts from a synchronised
+        // stream, and two plans within a few % of each other by the sum traded places as the
+        // bench's single timed call (65536^2 x 20: 2 x k_step_skew K = 10 vs 1 x k_step_tile
+        // K = 20, profiles/r03b_plan_choice.log).  So for every r the DP's plan, the best plan
+        // of each family alone and each family's single launch of depth r are timed as whole
+        // sequences the way gol_step runs them -- host wall time from a synchronised stream
+        // to the last launch's completion, best of 5, candidates interleaved -- and the
+        // fastest is kept in seq[r].
+        std::vector<std::vector<Launch>> seqs(kSeqMax + 1);
+        {
+            auto chain = [&](const std::vector<Launch> &pl, int r) {
+                std::vector<Launch> out;
+                for (int q = r; q >= 2 && pl[q].k >= 2; q -= pl[q].k) out.push_back(pl[q]);
+                int n = 0;
+                for (const Launch &L : out) n += L.k;
+                if (n != r) out.clear();
+                return out;
+            };
+            std::vector<std::vector<Launch>> fam_plan;
+            for (const Fam &f : fams) {
+                std::vector<float> cf(kSeqMax + 1, inf);
+                std::vector<Launch> pf(kSeqMax + 1, Launch{});
+                cf[0] = 0.f;
+                for (int r = 2; r <= kSeqMax; ++r)
+                    for (int k = 2; k <= std::min(r, golk::kMaxTurnsPerLaunch); ++k) {
+                        if (f.T[k] <= 0.f || r - k == 1 || cf[r - k] >= inf) continue;
+                        if (cf[r - k] + f.T[k] < cf[r]) {
+                            cf[r] = cf[r - k] + f.T[k];
+                            pf[r] = Launch{k, f.var, f.band_k[k], f.tw, f.seg};
+                        }
+                    }
+                fam_plan.push_back(std::move(pf));
+            }
+            auto same = [](const std::vector<Launch> &x, const std::vector<Launch> &y) {
+                if (x.size() != y.size()) return false;
+                for (size_t i = 0; i < x.size(); ++i)
+                    if (x[i].k != y[i].k || x[i].var != y[i].var || x[i].band != y[i].band ||
+                        x[i].tw != y[i].tw || x[i].seg != y[i].seg || x[i].blk != y[i].blk)
+                        return false;
+                return true;
+            };
+            auto time_seq = [&](const std::vector<Launch> &sq) -> float {
+                if (hipStreamSynchronize(c->stream) != hipSuccess) return 0.f;
+                const auto t0 = std::chrono::steady_clock::now();
+                bool ok = true;
+                int rep = 0;
+                for (const Launch &L : sq) {
+                    a.band = L.band;
+                    a.multi_variant = L.var == golk::kMultiTileStream ? golk::kMultiTile : L.var;
+                    a.tile_w = L.tw;
+                    a.tile_seg = L.seg;
+                    a.in = c->board[rep & 1];
+                    a.out = c->board[(rep + 1) & 1];
+                    ++rep;
+                    if (L.var == golk::kMultiTileStream)
+                        ok = ok && stream_launch(c, a, L.k, L.blk) == hipSuccess;
+                    else
+                        ok = ok && pg_prepare(c, a, L.k) == hipSuccess &&
+                             golk::launch_step_multi(a, L.k, c->stream) == hipSuccess;
+                }
+                ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
+                const std::chrono::duration<float, std::micro> d =
+                    std::chrono::steady_clock::now() - t0;
+                return ok ? d.count() : 0.f;
+            };
+            for (int r = 2; r <= kSeqMax; ++r) {
+                std::vector<std::vector<Launch>> cands;
+                auto add = [&](std::vector<Launch> sq) {
+                    if (sq.empty()) return;
+                    for (const auto &x : cands)
+                        if (same(x, sq)) return;
+                    cands.push_back(std::move(sq));
+                };
+                add(chain(plan, r));
+                // K1q (when tuned): the r turns as one launch of 2 or 3 near-equal blocks --
+                // shallower blocks carry fewer halo rows, and the launch starts only once
+                if (c->stream_k > 0)
+                    for (int nb : {2, 3}) {
+                        const int blk = (r + nb - 1) / nb;
+                        if (blk >= 4 && golk::tile_stream_ok(c->nw, c->buf_rows, blk, c->stream_th,
+                                                             c->stream_tw, c->stream_seg))
+                            add({Launch{r, golk::kMultiTileStream, c->stream_th, c->stream_tw,
+                                        c->stream_seg, blk}});
+                    }
+                for (size_t fi = 0; fi < fams.size(); ++fi) {
+                    add(chain(fam_plan[fi], r));
+                    if (r <= golk::kMaxTurnsPerLaunch && fams[fi].T[r] > 0.f)
+                        add({Launch{r, fams[fi].var, fams[fi].band_k[r], fams[fi].tw,
+                                    fams[fi].seg}});
+                }
+                if (cands.size() <= 1) {
+                    if (!cands.empty()) seqs[r] = cands[0];
+                    continue;
+                }
+                std::vector<float> tt(cands.size(), 0.f);
+                for (int pass = 0; pass < 5; ++pass)
+                    for (size_t i = 0; i < cands.size(); ++i) {
+                        const float v = time_seq(cands[i]);
+                        if (v > 0.f && (tt[i] == 0.f || v < tt[i])) tt[i] = v;
+                    }
+                size_t bi = 0;
+                for (size_t i = 1; i < cands.size(); ++i)
+                    if (tt[i] > 0.f && (tt[bi] == 0.f || tt[i] < tt[bi])) bi = i;
+                if (tt[bi] > 0.f) seqs[r] = cands[bi];
+                if (getenv("GOL_AUTOTUNE_LOG") && (r == 8 || r == 16 || r == 20 || r == 32))
+                    for (size_t i = 0; i < cands.size(); ++i) {
+                        fprintf(stderr, "autotune seq %d turns%s %.1f us =", r,
+                                i == bi ? " (pick)" : "", tt[i]);
+                        for (const Launch &L : cands[i])
+                            fprintf(stderr, " %d(var %d, band %d, tile %d,%d, blk %d)", L.k,
+                                    L.var, L.band, L.tw, L.seg, L.blk);
+                        fprintf(stderr, "\n");
+                    }
+            }
+        }
+        c->seq = std::move(seqs);
         if (getenv("GOL_AUTOTUNE_LOG")) {
             for (const Fam &f : fams)
                 for (int k = 2; k <= golk::kMaxTurnsPerLaunch; ++k)
