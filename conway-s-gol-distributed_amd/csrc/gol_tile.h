@@ -526,7 +526,8 @@ __global__ __launch_bounds__(1024, 1) void k_tile_persist(
 // i = b * ntiles + j is tile row (j / ntx + 2 b) mod nty, column j % ntx of block b: every
 // item of block b is taken before any of block b + 1, and an item waits only for its 8
 // neighbours' block b - 1 (flags as K1p: epoch + b once a tile's block-b stores completed),
-// which were taken earlier and so are running or done -- no deadlock whatever the residency.
+// and on its own block b - 1 (it ran on another workgroup), all taken earlier and so running
+// or done -- no deadlock whatever the residency.
 // Rotating the tile rows by 2 per block puts the first items of a block on rows whose
 // neighbours were among the first of the block before (the torus wrap would otherwise make
 // the first row wait for the previous block's last).  Block b reads u[(b-1) % 2] (block 0:
@@ -563,8 +564,11 @@ __global__ __launch_bounds__(1024, (SEG >= 20 ? 6 : 8)) void k_tile_stream(
         const int tile = ty * ntx + tx;
         const int k = kbase + (b < extra ? 1 : 0);
         if (b > 0) {
-            if (threadIdx.x < 8) {                        // one neighbour per lane 0..7
-                const int jj = (int)threadIdx.x + (threadIdx.x >= 4 ? 1 : 0);   // skip (0, 0)
+            // the 8 neighbours AND the tile itself: unlike K1p, the tile's own block b - 1 ran
+            // on some other workgroup, which may still be reading the buffer this item is about
+            // to overwrite, and wrote the interior this item reads
+            if (threadIdx.x < 9) {                        // one tile per lane 0..8
+                const int jj = (int)threadIdx.x;
                 const int dy = jj / 3 - 1, dx = jj % 3 - 1;
                 const int ny = (ty + dy + nty) % nty, nx = (tx + dx + ntx) % ntx;
                 const unsigned want = epoch + (unsigned)b;

@@ -16,3 +16,5 @@ step sweep65_s24 300 env GOL_STREAM=24 python -u tools/tile_sweep.py --size 6553
 step sweep65_s12 300 env GOL_STREAM=12 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 30:344:524:12,14:744:524:12
 step sweep16_s 300 env GOL_STREAM=32 python -u tools/tile_sweep.py --size 16384 --turns 640 --rounds 3 --shapes 14:316:106:32
 step auto65 400 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --auto
+step bench20_a 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1
+step bench1000 400 python -u bench.py --no-cpu-baseline --c2-size 0 --no-c1
