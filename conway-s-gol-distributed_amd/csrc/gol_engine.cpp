@@ -524,9 +524,7 @@ static hipError_t persist_buffers(gol_ctx *c, long long ntiles)
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return e;
     for (auto *&u : c->pu)
-        if (!u && (e = hipExtMallocWithFlags((void **)&u, words * 8, hipDeviceMallocUncached)) !=
-                      hipSuccess)
-            return e;
+        if (!u && (e = hipMalloc((void **)&u, words * 8)) != hipSuccess) return e;
     if (!c->pcounter) {
         if ((e = hipExtMallocWithFlags((void **)&c->pcounter, 64, hipDeviceMallocUncached)) !=
                 hipSuccess ||

@@ -8,7 +8,7 @@ step() { local name=$1 t=$2; shift 2
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
   echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log" | cut -c1-300
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc; }
-step stream_parity 300 python -u -m pytest tests/test_gpu_engine.py -q -x --timeout 150 --timeout-method thread -k "tile_stream_pinned"
+step stream_parity 300 python -u -m pytest tests/test_gpu_engine.py -q --timeout 150 --timeout-method thread -k "tile_stream_pinned or tile_persist_pinned"
 S65=30:335:524:20,14:713:524:24,30:536:524:20,30:344:524:12,14:744:524:12
 step sweep65_plain 300 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes $S65
 step sweep65_s20 300 env GOL_STREAM=20 python -u tools/tile_sweep.py --size 65536 --turns 480 --rounds 3 --shapes 30:335:524:20,30:536:524:20
