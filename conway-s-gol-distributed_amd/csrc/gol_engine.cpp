@@ -524,7 +524,9 @@ static hipError_t persist_buffers(gol_ctx *c, long long ntiles)
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return e;
     for (auto *&u : c->pu)
-        if (!u && (e = hipMalloc((void **)&u, words * 8)) != hipSuccess) return e;
+        if (!u && (e = hipExtMallocWithFlags((void **)&u, words * 8, hipDeviceMallocUncached)) !=
+                      hipSuccess)
+            return e;
     if (!c->pcounter) {
         if ((e = hipExtMallocWithFlags((void **)&c->pcounter, 64, hipDeviceMallocUncached)) !=
                 hipSuccess ||
@@ -1287,7 +1289,7 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
             const int N = 240;
             float sbest = 0.f;
             int sk = 0, sband = 0;
-            for (int Kp : {tf ? tf->K : 0, 12, 16, 20, 24, 32}) {
+            for (int Kp : {tf ? tf->K : 0, 24}) {
                 if (!tf || Kp < 2 || Kp > golk::kMaxTurnsPerLaunch || tf->band_k[Kp] <= 0)
                     continue;
                 // equal tile rows (the same count): a last tile row shorter than K would take

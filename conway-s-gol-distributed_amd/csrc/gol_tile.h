@@ -430,19 +430,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
         const int tr = t0 + i;
-        if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) {
-            if constexpr (PERSIST) {
-                // (write-through sc1 stores: the next block's readers on other XCDs load them
-                // with sc1 loads, which the XCD L2s serve -- no L2 holds a dirty copy)
-                if constexpr (W == 1)
-                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[i][0], v[i][1]}, rout, so, 0, 16);
-                else
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[i][0], v[i][1], v[i][2], v[i][3]},
-                                                           rout, so, 0, 16);
-            } else {
-                buf_store(v[i], rout, so, 0);
-            }
-        }
+        if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) buf_store(v[i], rout, so, 0);
         so += pitch_b;
     }
 }

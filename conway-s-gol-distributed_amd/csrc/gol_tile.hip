@@ -2,6 +2,8 @@
 #include "gol_tile.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <iterator>
 #include <map>
 #include <mutex>
@@ -238,9 +240,15 @@ hipError_t launch_tile_stream(const StepArgs &a, int turns, int K, uint64_t *u0,
     const int threads = 64 * tile_waves(K, a.band, a.tile_w, a.tile_seg);
     const size_t lds = tile_lds_bytes(threads, 1);
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess ||
-        per_cu < 1)
-        return hipErrorInvalidValue;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess)
+        per_cu = 0;
+    // (at least what k_step_tile gets with the same registers and LDS: a workgroup that does
+    // not fit yet just starts later and takes the items left then)
+    per_cu = std::max(per_cu, tile_blocks_per_cu(K, a.band, a.tile_w, a.tile_seg));
+    if (per_cu < 1) return hipErrorInvalidValue;
+    if (getenv("GOL_STREAM_LOG"))
+        fprintf(stderr, "k_tile_stream grid: %d CUs x %d workgroups of %d threads (occupancy API %d)\n",
+                ncu, per_cu, threads, [&] { int q = 0; (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, fn, threads, lds); return q; }());
     long long g = std::min<long long>(nitems, (long long)ncu * per_cu);
     if (max_grid > 0) g = std::min<long long>(g, max_grid);   // (tests: few workgroups)
     const unsigned grid = (unsigned)g;
