@@ -14,7 +14,7 @@ for r in rows:
     by[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k, c in by.items():
-    if "step" not in k:
+    if "step" not in k and "tile_stream" not in k and "tile_persist" not in k:
         continue
     m = {n: statistics.median(v) for n, v in c.items()}
     us = statistics.median(dur[k])
