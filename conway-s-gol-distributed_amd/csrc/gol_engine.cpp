@@ -2279,7 +2279,7 @@ int gol_tile_persist_codes(int32_t *codes, int32_t cap)
 
 int gol_tile_stream_codes(int32_t *codes, int32_t cap)
 {
-    const int n = (int)std::size(golk::kTileStreamCodes);
+    const int n = GOL_TOOLS ? (int)std::size(golk::kTileStreamCodes) : 0;   // (tools build)
     if (cap < 0 || (cap > 0 && !codes)) return GOL_EINVAL;
     for (int i = 0; i < std::min(n, (int)cap); ++i) codes[i] = golk::kTileStreamCodes[i];
     return n;

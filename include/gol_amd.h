@@ -178,7 +178,8 @@ int gol_tile_codes(int32_t *codes, int32_t cap);
  * across blocks of turns) runs; same convention. */
 int gol_tile_persist_codes(int32_t *codes, int32_t cap);
 /* The subset the streamed tile kernel (K1q: large torus boards, blocks of turns over
- * (block, tile) items taken in order by resident workgroups) runs; same convention. */
+ * (block, tile) items taken in order by resident workgroups) runs; same convention.  Empty
+ * in the product library (K1q is a tools-build experiment). */
 int gol_tile_stream_codes(int32_t *codes, int32_t cap);
 /* Lock-free progress read for a controlling thread: *turn = turns enqueued so far (the
  * board reaches it at the next gol_sync), *parked = 1 while gol_step is parked on PAUSE

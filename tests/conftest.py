@@ -32,8 +32,8 @@ TILE_CODES = (2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
               1204, 1206, 1208)
 
 
-# the subset the streamed tile kernel (K1q) runs (gol_tile_stream_codes)
-TILE_STREAM_CODES = (106, 506, 512, 524)
+# the subset the streamed tile kernel (K1q) runs (gol_tile_stream_codes): tools build only
+TILE_STREAM_CODES = (106, 506, 512, 524) if TOOLS_LIB else ()
 
 # the subset the persistent tile kernel (K1p) runs (gol_tile_persist_codes)
 TILE_PERSIST_CODES = (102, 103, 104, 106, 108, 112, 116, 403, 404, 406, 408, 412, 416,
