@@ -10,6 +10,7 @@ step() { local name=$1 t=$2; shift 2
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc; }
 step pmc_q 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so TAG=_q bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 20 --band 536 --tile 30,524 --stream 20 --turns 480
 step pmc_t 300 env TAG=_t bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 20 --band 536 --tile 30,524 --turns 480
+step k1q_debug 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/k1q_debug.py
 for t in _q _t; do for p in p1 p2; do
   f=$(ls gpurun_out/pmc_sq$t/$p/*counter_collection.csv 2>/dev/null | head -1)
   [ -n "$f" ] && python3 tools/pmc_report.py "$f" > gpurun_out/pmc_sq$t/${p}_report.txt
