@@ -583,6 +583,12 @@ __global__ __launch_bounds__(1024, (SEG >= 20 ? 6 : 8)) void k_tile_stream(
                 gave_up |= !seen;
             }
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            // cached block buffers (MI355X_MICROARCH, inter-workgroup visibility, consumer
+            // form): one agent acquire in the polling wave, its wait, then the barrier
+            if (threadIdx.x < 64) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __syncthreads();
         }
         const uint64_t *src = b == 0 ? in : ((b & 1) ? u0 : u1);
@@ -597,9 +603,13 @@ __global__ __launch_bounds__(1024, (SEG >= 20 ? 6 : 8)) void k_tile_stream(
         if (b + 1 < nblocks) {
             __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // this wave's stores are done
             __syncthreads();                                     // ... and every wave's
-            if (threadIdx.x == 0)
+            // (producer form: lane 0 writes the XCD L2's dirty lines back, waits, then flags)
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(flags + tile, epoch + (unsigned)b + 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (threadIdx.x == 0) next_item = nxt;
         __syncthreads();                                  // (and the LDS slots are free again)

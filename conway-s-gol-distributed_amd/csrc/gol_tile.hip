@@ -83,7 +83,7 @@ static void *tile_fn6(int seg)
 static void *stream_fn(int code)
 {
     static_assert(std::size(kTileStreamCodes) == 4, "stream_fn covers kTileStreamCodes");
-    if (!GOL_TOOLS) return nullptr;
+#if GOL_TOOLS
     switch (code) {
     case 106: return reinterpret_cast<void *>(&k_tile_stream<6, 1, 1>);
     case 506: return reinterpret_cast<void *>(&k_tile_stream<6, 5, 1>);
@@ -91,6 +91,10 @@ static void *stream_fn(int code)
     case 524: return reinterpret_cast<void *>(&k_tile_stream<24, 5, 1>);
     default: return nullptr;
     }
+#else
+    (void)code;
+    return nullptr;
+#endif
 }
 
 void *tile_kernel(int code)
