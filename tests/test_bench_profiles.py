@@ -27,7 +27,7 @@ def test_summary_matches_shape_exactly():
     other["tile"]["height_rows"] += 1
     assert b.pmc_summary(65536, 20, other) == (None, None)
     traffic, src = b.pmc_traffic(65536, 20, d["shape"])
-    assert traffic == d["traffic_bytes_per_launch"]
+    assert traffic == got["traffic_bytes_per_launch"]
 
 
 def test_every_r04_summary_has_one_kernel():
