@@ -137,6 +137,7 @@ struct gol_ctx {
     int stream_tw = 0, stream_th = 0, stream_seg = 0;
     unsigned *pcounter = nullptr;
     unsigned pcount = 0;
+    uint64_t *su[2] = {nullptr, nullptr};     // K1q block buffers (cached: hipMalloc)
     // device error word (host-mapped pinned memory; golk::kDevErr*): a k_step_wg wait that gave
     // up writes it, every synchronising call checks it
     unsigned *h_err = nullptr, *d_err = nullptr;
@@ -515,7 +516,7 @@ static hipError_t pg_prepare(gol_ctx *c, golk::StepArgs &a, int k)
     return hipSuccess;
 }
 
-// K1p / K1q: the block buffers (board-sized, cached), per-tile flags (uncached) and the item counter,
+// K1p / K1q: the uncached block buffers (board-sized), per-tile flags and the item counter,
 // allocated on first use (the engine's streams drained first)
 static hipError_t persist_buffers(gol_ctx *c, long long ntiles)
 {
@@ -523,8 +524,10 @@ static hipError_t persist_buffers(gol_ctx *c, long long ntiles)
     if (c->pu[0] && c->pu[1] && (size_t)ntiles <= c->pflags_n && c->pcounter) return hipSuccess;
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return e;
-    for (auto *&u : c->pu)     // (cached: the kernels hand blocks over with release / acquire)
-        if (!u && (e = hipMalloc((void **)&u, words * 8)) != hipSuccess) return e;
+    for (auto *&u : c->pu)
+        if (!u && (e = hipExtMallocWithFlags((void **)&u, words * 8, hipDeviceMallocUncached)) !=
+                      hipSuccess)
+            return e;
     if (!c->pcounter) {
         if ((e = hipExtMallocWithFlags((void **)&c->pcounter, 64, hipDeviceMallocUncached)) !=
                 hipSuccess ||
@@ -567,12 +570,18 @@ hipError_t stream_launch(gol_ctx *c, golk::StepArgs a, int turns, int K)
     const long long ntiles = golk::tile_count(c->nw, a.row_hi - a.row_lo, a.band, a.tile_w,
                                               a.tile_seg);
     if (hipError_t e = persist_buffers(c, ntiles)) return e;
+    for (auto *&u : c->su)
+        if (!u) {
+            hipError_t e = hipStreamSynchronize(c->stream);
+            if (e == hipSuccess) e = hipMalloc((void **)&u, (size_t)c->buf_rows * c->pitch * 8);
+            if (e != hipSuccess) return e;
+        }
     const unsigned nblocks = (unsigned)((turns + K - 1) / K);
     const unsigned epoch = c->pepoch + 1;
     unsigned grid = 0;
     // GOL_STREAM_GRID (tests): cap the workgroups, so that each takes many items
     const int max_grid = getenv("GOL_STREAM_GRID") ? atoi(getenv("GOL_STREAM_GRID")) : 0;
-    const hipError_t e = golk::launch_tile_stream(a, turns, K, c->pu[0], c->pu[1], c->pflags,
+    const hipError_t e = golk::launch_tile_stream(a, turns, K, c->su[0], c->su[1], c->pflags,
                                                   epoch, c->pcounter, c->pcount, c->ncu, max_grid,
                                                   &grid, c->stream);
     if (e != hipSuccess) return e;
@@ -1766,6 +1775,8 @@ void gol_destroy(gol_ctx *c)
         if (c->pg_rows) (void)hipFree(c->pg_rows);
         if (c->pg_flags) (void)hipFree(c->pg_flags);
         for (auto *u : c->pu)
+            if (u) (void)hipFree(u);
+        for (auto *u : c->su)
             if (u) (void)hipFree(u);
         if (c->pcounter) (void)hipFree(c->pcounter);
         if (c->pflags) (void)hipFree(c->pflags);

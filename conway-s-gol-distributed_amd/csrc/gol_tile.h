@@ -458,11 +458,9 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restric
 // launch (small boards: every tile is one resident workgroup, checked by the host).  A block
 // is one tile_pass; between blocks a tile exchanges its borders with its 8 neighbours through
 // memory instead of ending the launch: block b reads buffer u[(b-1) % 2] (block 0: `in`) and
-// writes u[b % 2] (the last block: `out`).  u0 / u1 are ordinary (cached) memory handed over
-// with the agent-scope release / acquire pair: the flag store follows a release (the XCD L2's
-// dirty lines written back), the poll an acquire (this CU's L1 invalidated), and the loads
-// are sc1 loads, which bypass the L1 as well.  (Uncached buffers, the first scheme, were
-// slower: 8-byte-per-lane, line-unaligned stores went to memory one by one.)  flags[tile] = epoch + b
+// writes u[b % 2] (the last block: `out`); u0 / u1 are uncached (visible across the XCDs' L2s
+// without cache maintenance, like the k_step_wg parallelogram rows) and read with sc1 loads
+// that bypass the CU's vector L1.  flags[tile] = epoch + b
 // + 1 once the tile's block-b stores completed; a tile starts block b when its 8 neighbours
 // are there -- which also means they finished reading the buffer it is about to overwrite.
 // A wait that gives up after kTileSpinLimit polls marks the error word (GOL_EHIP at the next
@@ -502,12 +500,6 @@ __global__ __launch_bounds__(1024, 1) void k_tile_persist(
             }
             // (the loads of the block stay below the waits: the barrier and the fence)
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            // cached block buffers: one agent acquire in the polling wave, its wait, then the
-            // barrier (MI355X_MICROARCH, inter-workgroup visibility, consumer form)
-            if (threadIdx.x < 64) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
             __syncthreads();
         }
         const uint64_t *src = b == 0 ? in : ((b & 1) ? u0 : u1);
@@ -516,14 +508,11 @@ __global__ __launch_bounds__(1024, 1) void k_tile_persist(
         if (b + 1 == nblocks) break;
         __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // this wave's stores are done
         __syncthreads();                                     // ... and every wave's
-        // (producer form: lane 0 writes the XCD L2's dirty lines back, waits, then flags;
-        // a workgroup-scope release would order nothing across CUs)
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // (u0 / u1 are uncached: completed stores are in memory; the flag is an agent-scope
+        // store, a workgroup-scope release would order nothing across CUs)
+        if (threadIdx.x == 0)
             __hip_atomic_store(flags + tile, epoch + (unsigned)b + 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
     if (gave_up && a.err)
         __hip_atomic_store(a.err, kDevErrTileFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
