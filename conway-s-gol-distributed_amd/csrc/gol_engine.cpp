@@ -1233,44 +1233,6 @@ void autotune_multi(gol_ctx *c, bool tune_k, bool tune_variant)
         }
     }
     if (pick_t > 0.f) best = pick_t;
-    // The ~1 ms timings above put a dozen candidates within ~1.5 % of each other, and the
-    // deepest-K rule then chose K = 32 on 512-row tiles (120.6k over 1000 turns at 65536^2,
-    // against 123k for K = 20-24 shapes; a tighter rule chose K1s K = 8, 119.5k).  So the
-    // candidates within 3 % of the best (at most 5, distinct) are timed again over >= ~240
-    // turns each, two interleaved passes, and the fastest of that is the steady-state pick.
-    if (pick_t > 0.f) {
-        std::vector<size_t> top;
-        std::vector<size_t> order(cand.size());
-        for (size_t i = 0; i < cand.size(); ++i) order[i] = i;
-        std::sort(order.begin(), order.end(), [&](size_t x, size_t y) {
-            const float tx = t[x] > 0.f ? t[x] : 1e30f, ty = t[y] > 0.f ? t[y] : 1e30f;
-            return tx < ty;
-        });
-        for (size_t i : order)
-            if (t[i] > 0.f && t[i] <= best * 1.03f && top.size() < 5) top.push_back(i);
-        if (top.size() > 1) {
-            std::vector<float> lt(top.size(), 0.f);
-            for (int pass = 0; pass < 2; ++pass)
-                for (size_t q = 0; q < top.size(); ++q) {
-                    const Cand &cd = cand[top[q]];
-                    const float v = time_one(cd, std::max(2, (240 + cd.K - 1) / cd.K));
-                    if (v > 0.f && (lt[q] == 0.f || v < lt[q])) lt[q] = v;
-                }
-            size_t bq = 0;
-            for (size_t q = 1; q < top.size(); ++q)
-                if (lt[q] > 0.f && (lt[bq] == 0.f || lt[q] < lt[bq])) bq = q;
-            if (getenv("GOL_AUTOTUNE_LOG"))
-                for (size_t q = 0; q < top.size(); ++q)
-                    fprintf(stderr, "autotune long %dx%d var=%d K=%d band=%d tile=%d,%d us_per_turn=%.3f%s\n",
-                            c->cfg.width, c->buf_rows, cand[top[q]].var, cand[top[q]].K,
-                            cand[top[q]].band, cand[top[q]].tw, cand[top[q]].seg, lt[q] * 1000.f,
-                            q == bq ? " (pick)" : "");
-            if (lt[bq] > 0.f) {
-                pick = cand[top[bq]];
-                best = pick_t = lt[bq];
-            }
-        }
-    }
     // Launch planner (tune_k and tune_variant only: nothing pinned).  For each kernel, its
     // fastest (K, band) is a family; time one launch of every family at every depth 2..16
     // (band_same_rounds), then plan, for every t <= kPlanMax turns, the sequence of launches
