@@ -179,11 +179,13 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
         runner = eng
         rows_local = H
         transport = ""
+        fallback = None
     else:
         eng = make_engine_strip(W, H, rank, world, a.halo, gpu, band_rows=a.band,
                                 turns_per_launch=a.tpl)
         eng.fill_random(seed)
         transport = a.transport
+        fallback = None
         if a.backend == "nccl" and transport == "rccl":
             from gol.rccl import RcclComm
             try:
@@ -193,6 +195,7 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
                     print(f"direct RCCL unavailable ({e}); using torch batch_isend_irecv",
                           file=sys.stderr)
                 comm, transport = None, "torch"
+                fallback = f"direct RCCL failed, fell back to torch batch_isend_irecv: {e}"[:300]
         runner = DistStrip(EngineStrip(eng, dev, stream), rank, world,
                            stage_on_host=a.backend == "gloo", rccl=comm,
                            overlap=bool(a.overlap))
@@ -242,7 +245,7 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
            "launches": launches, "K": info.turns_per_launch, "rows_local": rows_local,
            "band": info.band_rows, "fast": bool(info.fast_path), "halo": info.halo,
            "transport": transport, "overlap": overlap, "plan": plan, "tiles": tiles,
-           "seed": seed,
+           "seed": seed, "fallback": fallback,
            "exchanges": exchanges, "alive": alive}
     eng.close()
     return out
@@ -306,6 +309,7 @@ def config_entry(c, label, world, parallel):
          "valu_roofline_frac": round(g / world / VALU_PEAK_GCUPS, 4)}
     if world > 1:
         e["exchanges_timed"] = c["exchanges"]
+        e["transport_fallback"] = c.get("fallback")
     if c.get("alive") is not None:
         e["alive_cells_final"] = list(c["alive"])
     return e
@@ -516,6 +520,10 @@ def main():
                     "frac_at_measured_clock": round(per_gpu / pk, 4), "clock_source": src})
         if world > 1:
             out["config"]["exchanges_timed"] = m["exchanges"]
+            # which halo transport the timed region used, and why when it is not the requested
+            # one: a scaling run on the slower fallback transport must not pass unnoticed
+            out["config"]["halo_transport"] = m["transport"] if a.backend == "nccl" else "gloo"
+            out["config"]["transport_fallback"] = m["fallback"]
         cm = []
         if mx is not None:
             cm.append(config_entry(mx, f"{W}x{H} random torus board (seed {a.seed}), "

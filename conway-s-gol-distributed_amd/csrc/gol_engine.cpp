@@ -125,6 +125,7 @@ struct gol_ctx {
     // K1p (k_tile_persist, small torus boards): turns per block (0 = off), the uncached block
     // buffers and per-tile flags, and the flags' epoch (grows by blocks + 1 per launch)
     int persist_k = 0;
+    int persist_seg = 0;                     // K1p's segment code (plain launches keep tile_seg)
     bool persist_forced = false;             // GOL_PERSIST (tests): also on a shared device
     uint64_t *pu[2] = {nullptr, nullptr};
     unsigned *pflags = nullptr;
@@ -212,7 +213,7 @@ struct TuneKey {
     }
 };
 struct TuneVal {
-    int var, tpl, band, tile_w, tile_seg, persist_k;
+    int var, tpl, band, tile_w, tile_seg, persist_k, persist_seg;
     int stream_k, stream_tw, stream_th, stream_seg;
     float us;
     std::vector<Launch> plan;
@@ -423,7 +424,7 @@ Launch plan_launch(gol_ctx *c, int64_t room)
         const double us = c->tuned_us_per_turn > 0.f ? c->tuned_us_per_turn : 1.0;
         const int64_t cap = std::max<int64_t>(2 * c->persist_k, (int64_t)(1000.0 / us));
         return Launch{(int)std::min<int64_t>(room, cap), golk::kMultiTilePersist, c->band_multi,
-                      c->tile_w, c->tile_seg, c->persist_k};
+                      c->tile_w, c->persist_seg ? c->persist_seg : c->tile_seg, c->persist_k};
     }
     if (c->stream_k > 0 && !is_strip(c) && room >= 2 * c->stream_k) {
         // K1q: blocks of <= stream_k turns in one launch, up to ~8 ms of work per launch (the
@@ -696,6 +697,7 @@ void apply_tile(gol_ctx *c, const TileShape &t)
     c->plan.clear();
     c->seq.clear();
     c->persist_k = 0;
+    c->persist_seg = 0;
 }
 
 // Measured search for the k_step_tile shape (coordinate descent over the launch parameters;
@@ -949,6 +951,7 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
 void persist_tune(gol_ctx *c)
 {
     c->persist_k = 0;
+    c->persist_seg = 0;
     const bool log = getenv("GOL_AUTOTUNE_LOG") != nullptr;
     if (is_strip(c) || c->multi_variant != golk::kMultiTile || !device_exclusive(c->device) ||
         getenv("GOL_NO_PERSIST")) {
@@ -1039,7 +1042,7 @@ void persist_tune(gol_ctx *c)
     if (bad) clear_dev_err(c);
     if (best > 0.f && plain > 0.f && best < 0.98f * plain && !bad) {
         c->persist_k = best_k;
-        c->tile_seg = best_code;             // (short steps run plain launches of this code)
+        c->persist_seg = best_code;          // (plain launches keep the code they were timed at)
         c->tuned_us_per_turn = best;
     }
 }
@@ -1571,7 +1574,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     }
     if (const char *v = getenv("GOL_MULTI_VARIANT")) {    // A/B experiments only
         const int k = atoi(v);
-        const bool known = (k >= 0 && k < golk::kMultiCount) || k > golk::kMultiAblate;
+        const bool known = (k >= 0 && k < golk::kMultiUserEnd) || k > golk::kMultiAblate;
         // the product library ships only the kernels that compute the right board
         // (multi_variant_shipped); ablations, diagnostics and superseded variants need the
         // tools build (libgolamd_tools.so via GOL_AMD_LIB)
@@ -1723,6 +1726,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
             c->tile_w = v.tile_w;
             c->tile_seg = v.tile_seg;
             c->persist_k = v.persist_k;
+            c->persist_seg = v.persist_seg;
             c->stream_k = v.stream_k;
             c->stream_tw = v.stream_tw;
             c->stream_th = v.stream_th;
@@ -1743,7 +1747,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         if (use_cache) {
             std::lock_guard<std::mutex> lk(g_tune_mu);
             g_tune[key] = TuneVal{c->multi_variant, c->tpl, c->band_multi, c->tile_w,
-                                  c->tile_seg, c->persist_k, c->stream_k, c->stream_tw,
+                                  c->tile_seg, c->persist_k, c->persist_seg, c->stream_k, c->stream_tw,
                                   c->stream_th, c->stream_seg, c->tuned_us_per_turn, c->plan,
                                   c->seq};
         }
@@ -2280,7 +2284,7 @@ int gol_tile_codes(int32_t *codes, int32_t cap)
 
 int gol_tile_persist_codes(int32_t *codes, int32_t cap)
 {
-    const int n = (int)std::size(golk::kTilePersistCodes);
+    const int n = GOL_TOOLS ? (int)std::size(golk::kTilePersistCodes) : 0;   // (tools build)
     if (cap < 0 || (cap > 0 && !codes)) return GOL_EINVAL;
     for (int i = 0; i < std::min(n, (int)cap); ++i) codes[i] = golk::kTilePersistCodes[i];
     return n;

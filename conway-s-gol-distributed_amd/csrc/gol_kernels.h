@@ -74,13 +74,20 @@ enum : int {
     kMultiWgPgS = 14,       // kMultiWgPg, stages in order (band rule: golk::pg_ok(.., true))
     kMultiTile = 15,        // k_step_tile: a 2-D tile per workgroup, resident in registers for
                             //   all K turns (small boards: gol_tile.h)
-    kMultiCount = 16,
+    kMultiUserEnd = 16,     // variants 0 .. kMultiUserEnd - 1 may be requested (GOL_MULTI_VARIANT);
+                            //   the ids from here on are engine-internal launch kinds
     kMultiTilePersist = 16, // K1p k_tile_persist: k_step_tile's tiles resident across blocks of
-                            //   K turns (engine-internal: small torus boards, never requested)
+                            //   K turns (engine-internal; tools build only)
     kMultiTileStream = 17,  // K1q k_tile_stream: blocks of K turns over (block, tile) items taken
-                            //   in order by resident workgroups (engine-internal, large boards)
+                            //   in order by resident workgroups (engine-internal; tools build only)
+    kMultiInternalEnd = 18, // one past the engine-internal launch kinds (size of any table by kind)
     kMultiAblate = 100,     // 100 + ABL mask: k_step_skew<8> timing ablations (K = 8 only)
 };
+
+static_assert(kMultiTile < kMultiUserEnd && kMultiWgPgS < kMultiUserEnd,
+              "every requestable variant lies below the engine-internal launch kinds");
+static_assert(kMultiTilePersist >= kMultiUserEnd && kMultiTileStream < kMultiInternalEnd &&
+              kMultiInternalEnd < kMultiAblate, "engine-internal kinds between the two ranges");
 
 #ifndef GOL_TOOLS
 #define GOL_TOOLS 0   // 1: the tools build (libgolamd_tools.so, see the Makefile)
@@ -203,8 +210,10 @@ constexpr int kTileCodes[] = {
     1102, 1103, 1104, 1106, 1108,
     1204, 1206, 1208,
 };
-// the codes k_tile_persist (K1p) is instantiated for (gol_tile.hip persist_fn; each pinned by
-// tests/test_gpu_engine.py::test_tile_persist_pinned through gol_tile_persist_codes)
+// the codes k_tile_persist (K1p) is instantiated for in the tools build (gol_tile.hip
+// persist_fn; each pinned by tests/test_gpu_engine.py::test_tile_persist_pinned through
+// gol_tile_persist_codes, which reports none in the product library: K1p never won its
+// autotune and its uncached hand-off shares K1q's unexplained wrong-board runs)
 constexpr int kTilePersistCodes[] = {102, 103, 104, 106, 108, 112, 116,
                                      403, 404, 406, 408, 412, 416,
                                      2, 3, 4, 6, 8,

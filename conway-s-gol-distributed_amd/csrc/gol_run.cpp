@@ -224,11 +224,6 @@ struct gol_run {
         closed = true;
         cv_pop.notify_all();
     }
-    bool has_key()
-    {
-        std::lock_guard<std::mutex> lk(kmu);
-        return !keys.empty();
-    }
     bool pop_key(int &k)
     {
         std::lock_guard<std::mutex> lk(kmu);
@@ -541,8 +536,7 @@ void gol_run::run()
     }
 
     auto next_tick = Clock::now() + std::chrono::milliseconds(ticker_ms);
-    auto tick = [&]() -> bool {
-        if (Clock::now() < next_tick) return true;
+    auto tick_now = [&]() -> bool {                   // the tick that is due, unconditionally
         next_tick += std::chrono::milliseconds(ticker_ms);
         long long t = 0, a = 0;
         if (st.snapshot(t, a)) { die(st.err); return false; }
@@ -550,6 +544,7 @@ void gol_run::run()
         e.cells_count = a;
         return send(e);
     };
+    auto tick = [&]() -> bool { return Clock::now() < next_tick || tick_now(); };
     auto save_image = [&](long long t) -> bool {      // 's' and the final output
         HostBuf out;
         if (st.read_board(out)) { die(st.err); return false; }
@@ -628,11 +623,16 @@ void gol_run::run()
         // re-arm before draining the keys: a key pushed from here on stops the next chunk
         if (!st.strip_mode()) (void)gol_set_control(st.eng[0], GOL_CONTROL_RUN);
         int k;
-        if (has_key()) {                              // keys see every enqueued turn done
-            if (!retire(0)) return close();
-            if (st.sync()) return die(st.err);
-        }
+        bool drained = false;
         while (!quit && pop_key(k)) {
+            // a key sees every enqueued turn done, and its events follow their TurnComplete
+            // events: drain after the pop (checking for a key first and popping later let a key
+            // that arrived in between be served with the previous chunk still in flight)
+            if (!drained) {
+                if (!retire(0)) return close();
+                if (st.sync()) return die(st.err);
+                drained = true;
+            }
             if (k == 's') {                           // distributor.go:131-144
                 if (!save_image(turn)) return close();
             } else if (k == 'q' || k == 'k') {        // :113-115, :146-150
@@ -658,8 +658,10 @@ void gol_run::run()
             }
         }
         if (quit) break;
-        if (Clock::now() >= next_tick && !retire(0)) return close();
-        if (!tick()) return close();
+        if (Clock::now() >= next_tick) {              // one clock read decides: drain, then tick
+            if (!retire(0)) return close();
+            if (!tick_now()) return close();
+        }
 
         const long long want = std::min(chunk, p.turns - turn);
         const auto t0 = Clock::now();

@@ -34,10 +34,17 @@ static void *tile_fn(int seg)
 }
 
 // k_tile_persist instantiations (K1p, small boards): one word per lane; in order (ORD 0),
-// interior rows first with the workgroup barrier (ORD 1, 5) or with neighbour flags (ORD 4)
+// interior rows first with the workgroup barrier (ORD 1, 5) or with neighbour flags (ORD 4).
+// Tools build only (round 5): K1p never won its own autotune (5120^2: 0.588 against 0.563 us
+// per turn for plain launches, profiles/r04_c2_autotune_persist.log), and its uncached
+// block hand-off is the scheme under which K1q computed wrong boards with the cause unknown.
 static void *persist_fn(int code)
 {
     static_assert(std::size(kTilePersistCodes) == 22, "persist_fn covers kTilePersistCodes");
+#if !GOL_TOOLS
+    (void)code;
+    return nullptr;
+#else
     switch (code) {
     case 102: return reinterpret_cast<void *>(&k_tile_persist<2, 1, 1>);
     case 103: return reinterpret_cast<void *>(&k_tile_persist<3, 1, 1>);
@@ -63,6 +70,7 @@ static void *persist_fn(int code)
     case 508: return reinterpret_cast<void *>(&k_tile_persist<8, 5, 1>);
     default: return nullptr;
     }
+#endif
 }
 
 // ORD 6 (the barrier after the interior rows, edge sums read back): the 6-8 waves per SIMD

@@ -28,7 +28,35 @@ _UID_BYTES = 128                    # NCCL_UNIQUE_ID_BYTES
 
 
 class _UniqueId(ctypes.Structure):
-    _fields_ = [("internal", ctypes.c_char * _UID_BYTES)]
+    # c_ubyte, not c_char: a c_char array field reads back as a NUL-terminated string, and an
+    # RCCL unique id ({uint64 magic; sockaddr root}) holds NULs from byte 2 of the sockaddr on
+    # (AF_INET = 02 00), so a c_char field cut every id before the root's port and address
+    _fields_ = [("internal", ctypes.c_ubyte * _UID_BYTES)]
+
+
+def uid_to_bytes(uid: _UniqueId) -> bytes:
+    """All NCCL_UNIQUE_ID_BYTES bytes of ``uid``, NULs included."""
+    return ctypes.string_at(ctypes.addressof(uid), _UID_BYTES)
+
+
+def uid_from_bytes(data) -> _UniqueId:
+    """A unique id holding exactly ``data`` (NCCL_UNIQUE_ID_BYTES bytes)."""
+    data = bytes(data)
+    if len(data) != _UID_BYTES:
+        raise ValueError(f"unique id must be {_UID_BYTES} bytes, got {len(data)}")
+    uid = _UniqueId()
+    ctypes.memmove(ctypes.addressof(uid), data, _UID_BYTES)
+    return uid
+
+
+def broadcast_unique_id(uid: _UniqueId, group=None, where="cpu") -> _UniqueId:
+    """Rank 0's ``uid`` on every rank of ``group`` (a collective: every rank calls it; the
+    other ranks' ``uid`` is ignored).  ``where`` is the device the group's backend moves
+    tensors on ("cpu" for gloo, the rank's GPU for nccl).  Byte-exact: the id travels as a
+    128-element uint8 tensor, never as a string."""
+    t = torch.tensor(list(uid_to_bytes(uid)), dtype=torch.uint8, device=where)
+    dist.broadcast(t, src=0, group=group)
+    return uid_from_bytes(bytes(t.cpu().tolist()))
 
 
 _lib = None
@@ -95,10 +123,7 @@ class RcclComm:
             if int(ok.item()) == 0:
                 raise RuntimeError(f"rank {self.rank}: direct RCCL unavailable on some rank"
                                    + (f" ({err})" if err else ""))
-            t = torch.frombuffer(bytearray(bytes(uid.internal).ljust(_UID_BYTES, b"\0")),
-                                 dtype=torch.uint8).clone().to(where)
-            dist.broadcast(t, src=0, group=group)
-            uid.internal = bytes(t.cpu().tolist())
+            uid = broadcast_unique_id(uid, group, where)
         elif err is not None:
             raise RuntimeError(f"direct RCCL unavailable ({err})")
         with torch.cuda.device(device):

