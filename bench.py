@@ -246,10 +246,15 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
            "band": info.band_rows, "fast": bool(info.fast_path), "halo": info.halo,
            "transport": transport, "overlap": overlap, "plan": plan, "tiles": tiles,
            "seed": seed, "fallback": fallback,
+           "shape_source": SHAPE_SOURCES.get(int(info.shape_source), "?"),
            "exchanges": exchanges, "alive": alive}
     eng.close()
     return out
 
+
+# gol_info.shape_source: where the launch shape the timed region ran came from
+SHAPE_SOURCES = {0: "defaults", 1: "create-time timing search",
+                 2: "pinned MI355X shape table (gol_engine.cpp kKnownShapes)"}
 
 KERNELS = {16: "k_tile_persist<K> (k_step_tile's 2-D tiles resident across blocks of turns)",
            17: "k_tile_stream<K> (k_step_tile's 2-D tiles in blocks of turns, items taken in "
@@ -301,7 +306,7 @@ def config_entry(c, label, world, parallel):
     e = {"workload": label, "value": round(g, 2), "unit": "GCUPS", "n_gpus": world,
          "ms_per_step": round(c["wall"] * 1e3 / c["steps"], 6), "parallelism": parallel,
          "band_rows": shape.get("band_rows", c["band"]), "temporal_blocking_k": kd,
-         "launch_shape": shape,
+         "launch_shape": shape, "shape_source": c.get("shape_source"),
          "kernel": KERNELS.get(kvar, f"kernel {kvar}").replace("<K>", f"<K={kd}>"),
          "launch_plan": text[:300], "traffic": traffic, "traffic_source": src,
          "launch_us": round(lu, 3), "launches": c["launches"],
@@ -477,7 +482,7 @@ def main():
                        "parallelism": parallelism(a, world, m),
                        "band_rows": shape.get("band_rows", m["band"]), "fast_path": m["fast"],
                        "temporal_blocking_k": kdepth,
-                       "launch_shape": shape,
+                       "launch_shape": shape, "shape_source": m["shape_source"],
                        "launch_plan": plan_text},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -89,6 +89,7 @@ struct gol_ctx {
     long long last_n = 0;
     int ncu = 0;                             // compute units of the device
     float tuned_us_per_turn = 0.f;           // autotune's best measurement (0 = not tuned)
+    int shape_source = 0;                    // gol_info.shape_source: 1 = searched, 2 = kKnownShapes
     uint64_t *board[2] = {nullptr, nullptr};
     int cur = 0;
     bool il = false;                         // board[cur] is in the interleaved layout
@@ -941,6 +942,48 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     return pick;
 }
 
+// Pinned launch shapes for the BASELINE board sizes on an MI355X (gfx950, 256 CUs): a torus
+// engine of one of these sizes with nothing pinned by the caller runs this k_step_tile shape
+// and skips the create-time search.  The search's 0.5 ms timings put a dozen shapes within
+// ~1.5 % of each other and picked different ones from box to box (round 4: 65536^2 K = 20 on
+// 336-row tiles on one box, K = 32 on 512-row tiles or k_step_skew K = 8 on others; 16384^2
+// bands 316 / 320), so the kernel a bench line timed was not reliably the one profiles/
+// measured.  These are the search winners of the round-4 sweeps, each pinned by a full-size
+// oracle digest (tests/test_gpu_engine.py::test_pinned_shape_digest) and profiled as is
+// (profiles/r05_*_summary.json).  GOL_AUTOTUNE=2 measures instead.
+struct KnownShape {
+    int width, rows;
+    TileShape t;                             // K, tile height, tile width (lanes), segment code
+    float us_per_turn;                       // measured steady state (round-4 sweeps)
+};
+constexpr KnownShape kKnownShapes[] = {
+    // configs[3..4]: ORD 5, SEG 24, 8-wave workgroups (6 waves per SIMD); 34.5-34.7 us per turn
+    // (profiles/r04_sweep_65536_ord5.log, r04_sweep_65536_fine.log); the driver's 20-turn call
+    // is one launch of this shape
+    {65536, 65536, {20, 336, 30, 524, 0}, 34.6f},
+    // configs[2]: ORD 1, SEG 6, 16-wave workgroups (8 waves per SIMD), two residency rounds;
+    // 2.94-3.02 us per turn (BENCH_r04 configs_measured)
+    {16384, 16384, {32, 316, 14, 106, 0}, 2.96f},
+    // configs[1]: ORD 2, SEG 3, 16-wave workgroups; 0.57-0.59 us per turn (BENCH_r04)
+    {5120, 5120, {32, 128, 14, 203, 0}, 0.58f},
+};
+
+bool known_shape(const gol_ctx *c, KnownShape *out)
+{
+    if (c->ncu != 256 || is_strip(c)) return false;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess ||
+        std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return false;
+    for (const KnownShape &k : kKnownShapes)
+        if (k.width == c->cfg.width && k.rows == c->buf_rows &&
+            golk::tile_shape_ok(c->nw, k.t.K, k.t.th, k.t.tw, k.t.seg)) {
+            *out = k;
+            return true;
+        }
+    return false;
+}
+
 // Boards below 2^20 words (5120^2: 409 600) cannot fill the GPU with band pipelines: they run
 // k_step_tile at the measured-best shape.
 // K1p for a small torus board at the tuned tile shape: 256 turns as one k_tile_persist launch
@@ -1701,8 +1744,17 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         }
     }
     const char *at = getenv("GOL_AUTOTUNE");
-    const bool tuning = !(cfg->flags & GOL_FLAG_NO_AUTOTUNE) && (!at || atoi(at) != 0) &&
-                        cfg->band_rows <= 0 && c->tpl > 1;
+    bool tuning = !(cfg->flags & GOL_FLAG_NO_AUTOTUNE) && (!at || atoi(at) != 0) &&
+                  cfg->band_rows <= 0 && c->tpl > 1;
+    // a BASELINE board size on an MI355X: the pinned shape, no search (GOL_AUTOTUNE=2: search)
+    KnownShape ks{};
+    if (tuning && !pinned && cfg->turns_per_launch <= 0 && !getenv("GOL_TILE") &&
+        !(at && atoi(at) == 2) && known_shape(c, &ks)) {
+        apply_tile(c, ks.t);
+        c->tuned_us_per_turn = ks.us_per_turn;
+        c->shape_source = 2;
+        tuning = false;
+    }
     const bool tune_small = small && c->multi_variant == golk::kMultiTile && !pinned &&
                             cfg->turns_per_launch <= 0;
     // the kernel is tuned too unless an experiment pins it (GOL_MULTI_VARIANT) or the requested
@@ -1735,12 +1787,14 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
             c->seq = v.seq;
             c->tuned_us_per_turn = v.us;
             for (int &b : c->band_at) b = 0;
+            c->shape_source = 1;
             cached = true;
         }
     }
     if (tuning && !cached && (tune_small || !small)) {
         if (tune_small) autotune_small(c);
         else autotune_multi(c, cfg->turns_per_launch <= 0, tune_var);
+        c->shape_source = 1;
         // a wait that gave up while timing the candidates: fail loudly at create
         (void)hipStreamSynchronize(c->stream);
         if (check_dev_err(c)) return bail(GOL_EHIP);
@@ -1819,6 +1873,7 @@ int gol_get_info(gol_ctx *c, gol_info *info)
         info->nonbinary_cells = c->nonbinary;
         info->launches = c->launches;
         info->blocking_limited = c->blocking_limited ? 1 : 0;
+        info->shape_source = c->shape_source;
         return GOL_OK;
     });
 }

@@ -65,7 +65,8 @@ class gol_info(ctypes.Structure):
                 ("halo_valid", ctypes.c_int32), ("turns_per_launch", ctypes.c_int32),
                 ("device", ctypes.c_int32),
                 ("turn", ctypes.c_int64), ("nonbinary_cells", ctypes.c_int64),
-                ("launches", ctypes.c_int64), ("blocking_limited", ctypes.c_int32)]
+                ("launches", ctypes.c_int64), ("blocking_limited", ctypes.c_int32),
+                ("shape_source", ctypes.c_int32)]
 
 
 class gol_params(ctypes.Structure):

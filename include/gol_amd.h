@@ -104,6 +104,10 @@ typedef struct gol_info {
     int32_t  blocking_limited;  /* 1 = temporal blocking is off because a board buffer is
                                    >= 2 GiB (the multi-turn kernel's 32-bit buffer offsets):
                                    every launch runs one turn                          */
+    int32_t  shape_source;      /* where the multi-turn launch shape came from: 0 = defaults
+                                   or the caller (gol_config / GOL_* experiments), 1 = the
+                                   create-time timing search, 2 = the pinned table of
+                                   MI355X shapes for the BASELINE board sizes            */
 } gol_info;
 
 /* Whole-board (torus) engine on the current device. */

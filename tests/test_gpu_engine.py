@@ -518,16 +518,20 @@ def test_large_board_digests(gol, key):
         assert hashlib.sha256(words.tobytes()).hexdigest() == d["sha256"]
 
 
-@pytest.mark.parametrize("pin", [None, "tile"])
+@pytest.mark.parametrize("pin", [None, "tile", "search"])
 def test_driver_command_digest(gol, monkeypatch, pin):
     """The driver's bench command at the headline size (bench.py --steps 20 --warmup 5):
     65536^2 seed 3, one gol_step of 5 turns, then one of 20, against the oracle digest of 25
-    turns -- with the plan the engine tunes for itself, and with the 20-turn launch pinned to
-    the k_step_tile shape the bench profiles (Measurement)."""
+    turns -- with the engine's own choice (the pinned MI355X shape: one k_step_tile launch of
+    20 turns on 30 x 336 tiles of ORD 5 SEG 24, code 524, the launch BENCH_r04 timed), with
+    that launch forced through GOL_TILE, and with the create-time search (GOL_AUTOTUNE=2)."""
     if pin == "tile":
         monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
-        monkeypatch.setenv("GOL_TILE", "14,116")
-        kw = dict(band_rows=960, turns_per_launch=20)
+        monkeypatch.setenv("GOL_TILE", "30,524")
+        kw = dict(band_rows=336, turns_per_launch=20)
+    elif pin == "search":
+        monkeypatch.setenv("GOL_AUTOTUNE", "2")
+        kw = {}
     else:
         kw = {}
     d = _digests()["65536x65536_seed3_t25"]
@@ -535,9 +539,41 @@ def test_driver_command_digest(gol, monkeypatch, pin):
         e.fill_random(d["seed"])
         e.step(5)
         e.step(20)
-        if pin == "tile":
-            assert [(k, v) for k, v, _ in e.last_launches()] == [(20, 15)]
+        if pin != "search":
+            assert [(k, v, b) for k, v, b in e.last_launches()] == [(20, 15, 336)]
+            assert [(t[0], t[1]) for t in e.last_launch_tiles(blocks=True)] == [(30, 524)]
+        assert e.info().shape_source == {None: 2, "tile": 0, "search": 1}[pin]
         assert e.snapshot() == (25, d["alive"])
+        assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
+
+
+# the pinned MI355X launch shapes (gol_engine.cpp kKnownShapes): board -> (K, tile height, tile
+# width in lanes, segment code); the bench's configs run exactly these, and profiles/ has a
+# kernel-trace + PMC summary of each
+PINNED_SHAPES = {65536: (20, 336, 30, 524), 16384: (32, 316, 14, 106), 5120: (32, 128, 14, 203)}
+
+
+@pytest.mark.parametrize("key", ["65536x65536_seed3_t1000", "16384x16384_seed2_t10000",
+                                 "5120x5120_seed1_t1000"])
+def test_pinned_shape_digest(gol, key):
+    """Each BASELINE board size runs its pinned shape (no create-time search: the kernel the
+    bench times is the one profiles/ measured, on every box) and matches the oracle's
+    full-size digest: 65536^2 x 1000 (configs[3], 50 launches of K = 20), 16384^2 x 10000
+    (configs[2], K = 32 on 14 x 316 tiles of ORD 1 SEG 6), 5120^2 x 1000 (configs[1], K = 32
+    on 14 x 128 tiles of ORD 2 SEG 3)."""
+    d = _digests()[key]
+    K, th, tw, code = PINNED_SHAPES[d["width"]]
+    with _engine(gol, d["width"], d["height"]) as e:
+        info = e.info()
+        assert info.shape_source == 2 and info.turns_per_launch == K and info.band_rows == th
+        e.fill_random(d["seed"])
+        e.step(d["turns"])
+        plan = e.last_launches()
+        tiles = e.last_launch_tiles(blocks=True)
+        assert {(v, b) for _, v, b in plan} == {(15, th)}
+        assert max(k for k, _, _ in plan) == K and sum(k for k, _, _ in plan) == d["turns"]
+        assert {(t[0], t[1]) for t in tiles} == {(tw, code)}
+        assert e.snapshot() == (d["turns"], d["alive"])
         assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
 
 

@@ -450,7 +450,7 @@ def test_stub_harness_no_tick_after_quitting(workdir, monkeypatch):
     series = G.alive_series(512)
     ticks_seen = 0
     for _ in range(3):
-        s = Stub(workdir, 512, 4000, 5)
+        s = Stub(workdir, 512, 1000000, 5)          # (~0.15 s of stepping: ~3 ticks)
         evs = list(s.events())
         s.wait()
         names = [e[0] for e in evs]

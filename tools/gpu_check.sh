@@ -19,7 +19,6 @@ for step in "$@"; do
     smoke)  run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 300 python -u bench.py --steps 200 --no-cpu-baseline ;;
     benchfull) run benchfull 400 python -u bench.py ;;
-    profile) run profile 800 bash tools/profile.sh ;;
     tb)     run tb 500 python -u tools/sweep.py --variants 2 --bands 32,64,128 --tpl 1,3,4,5,6,8 --mw 1,2 --turns 120 ;;
     tb16k)  run tb16k 300 python -u tools/sweep.py --size 16384 --variants 2 --bands 8,16,32 --tpl 1,3,4,5,6,8 --mw 1,2 --turns 960 ;;
     pmcsq)  run pmcsq 300 bash tools/pmc_sq.sh ;;
@@ -43,12 +42,13 @@ for step in "$@"; do
     c2def)  run c2def 300 python -u bench.py --size 5120 --steps 1000 --warmup 40 --c3-size 0 --no-cpu-baseline ;;
     c2sweep) run c2sweep 500 python -u tools/sweep.py --size 5120 --variants 2 --bands 16,24,32,48,64 --tpl 4,8,12,16 --mw 1 --mv 7,9,12 --turns 960 ;;
     sq65)   run sq65 300 bash tools/pmc_sq.sh ;;
+    prof)   run prof 1100 bash tools/profile_bench.sh ;;
+    fullnx) run fullnx 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
     nobar)  run nobar 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 5120 --turns 960 --rounds 3 --shapes 30:64:8:32,30:64:308:32,30:64:4:32,30:64:304:32,10:160:4:32,10:160:304:32 && run nobar16 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 16384 --turns 320 --rounds 3 --shapes 29:320:24:32,29:320:324:32 ;;
     sqc2)   run sqc2 300 env TAG=_c2 bash tools/pmc_sq.sh tools/kernel_run.py --size 5120 --mv 15 --tpl 32 --band 160 --tile 10,4 --turns 3200 && run sqc3 300 env TAG=_c3 bash tools/pmc_sq.sh tools/kernel_run.py --size 16384 --mv 15 --tpl 32 --band 320 --tile 29,124 --turns 640 ;;
     bench2g) run bench2g 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --backend gloo --c3-size 4096 --c3-turns 300 ;;
-    prof3)  run prof3 1000 bash tools/profile_r03.sh ;;
     bench20) run bench20 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     newt)   run newt 400 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "tile or small_board or rejects_tools or spin_timeout or snapshot_while or control_word or 5120 or random_vs_oracle" ;;
     c2tile) run c2tile 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --shapes 10:160:4:32,10:160:4:16,10:160:3:24,10:160:8:32,10:80:4:16,10:80:2:12,16:160:4:24,14:160:4:24,20:320:4:32,10:160:12:32,10:320:16:32,30:320:16:16,10:96:2:32,10:128:2:16,10:64:2:16,10:160:2:24,14:128:2:16,6:128:3:16,6:96:2:16 ;;
@@ -61,18 +61,12 @@ for step in "$@"; do
     bigtile65) run bigtile65 300 python -u tools/tile_sweep.py --size 65536 --turns 64 --rounds 2 --shapes 62:576:40:32,30:576:40:32,62:448:32:32,14:900:16:24,62:700:48:16 ;;
     tilesw5) run tilesw5 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --shapes 10:160:4:32,10:128:4:32,30:64:8:32,30:64:208:32,14:128:106:32,10:160:106:32,10:96:4:24 ;;
     tilesw16) run tilesw16 300 env GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 16384 --auto --turns 960 --shapes 29:320:24:32,29:320:124:32,29:320:224:32 ;;
-    ab16) run ab16_old 200 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_old.so python -u tools/tile_sweep.py --size 16384 --turns 960 --shapes 29:320:24:32,29:320:124:32 && run ab16_new 200 python -u tools/tile_sweep.py --size 16384 --turns 960 --shapes 29:320:24:32,29:320:124:32 && run ab5_old 200 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_old.so python -u tools/tile_sweep.py --size 5120 --turns 960 --shapes 10:160:4:32,14:128:106:32 && run ab5_new 200 python -u tools/tile_sweep.py --size 5120 --turns 960 --shapes 10:160:4:32,14:128:106:32 ;;
-    abx) run abx16 500 env LIBS="old new exp2" bash tools/ab_tile.sh 16384 640 29:320:24:32,29:320:124:32,14:320:106:32 && run abx65 500 env LIBS="old new exp2" bash tools/ab_tile.sh 65536 64 30:576:40:32,30:576:140:32 && run abx5 300 env LIBS="old new exp2" bash tools/ab_tile.sh 5120 960 10:160:4:32,14:128:103:32 ;;
-    aby) run aby16 500 env LIBS="old new old new" bash tools/ab_tile.sh 16384 640 29:320:124:32,14:320:106:32 && run aby65 500 env LIBS="old new old new" bash tools/ab_tile.sh 65536 64 30:576:140:32 && run aby5 300 env LIBS="old new" bash tools/ab_tile.sh 5120 960 10:160:4:32,14:128:103:32 ;;
     small65) run small65 400 python -u tools/tile_sweep.py --size 65536 --turns 96 --rounds 2 --shapes 30:576:140:32,14:320:106:32,14:352:106:16,14:336:106:24,14:352:206:16,14:224:104:16,14:352:6:16,10:256:104:32,10:288:104:16 && run small8448 400 python -u tools/tile_sweep.py --size 65536 --height 8448 --turns 192 --rounds 2 --shapes 62:192:132:32,14:320:106:32,14:352:106:16,14:336:106:24,14:352:206:16,14:224:104:16,14:352:6:16,10:288:104:16 ;;
     sqb) run sqc2b 300 env TAG=_c2b bash tools/pmc_sq.sh tools/kernel_run.py --size 5120 --mv 15 --tpl 32 --band 128 --tile 14,103 --turns 3200 && run sqc3b 300 env TAG=_c3b bash tools/pmc_sq.sh tools/kernel_run.py --size 16384 --mv 15 --tpl 32 --band 320 --tile 14,106 --turns 640 ;;
     kfix) run kfix 300 python -u tools/tile_sweep.py --size 5120 --turns 960 --rounds 2 --shapes 14:128:104:2,14:128:104:4,14:128:104:8,14:128:104:16,14:128:104:32,14:128:103:32,14:128:103:16 && run kfix16 300 python -u tools/tile_sweep.py --size 16384 --turns 640 --rounds 2 --shapes 14:320:106:2,14:320:106:4,14:320:106:8,14:320:106:16,14:320:106:32 ;;
-    prof3b) run prof3b 800 bash tools/profile_r03b.sh ;;
-    prof3bk) run prof3bk 500 env ONLY_K20=1 bash tools/profile_r03b.sh ;;
     k20) run k20 400 python -u tools/tile_sweep.py --size 65536 --turns 80 --rounds 3 --shapes 14:960:116:20,14:960:16:20,14:984:16:20,14:960:216:20,30:600:140:20,30:600:40:20,14:448:8:20,14:448:108:20,14:960:16:32,30:576:140:32 ;;
     warm) for w in 5 60 5; do run warm$w 200 python -u bench.py --gpus 1 --steps 20 --warmup $w --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done; run warm40 200 python -u bench.py --gpus 1 --steps 40 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 ;;
     ovl8) run ovl8 400 python -u tools/strip_emulate.py --n 8,4 --halo 128 --rccl direct --turns 768 && run ovl8o 400 python -u tools/strip_emulate.py --n 8,4 --halo 128 --rccl direct --overlap --turns 768 ;;
-    pairs) run pairs16 400 env LIBS="new p7 p16 new" bash tools/ab_tile.sh 16384 640 14:448:208:32,14:448:108:32,14:704:112:32,14:960:116:32 && run pairs65 500 env LIBS="new p7 p16" bash tools/ab_tile.sh 65536 80 14:960:116:20,14:448:108:32 ;;
     cold) run coldt 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "planner or interleaved or control_word or snapshot" && run coldb 300 env GOL_AUTOTUNE_LOG=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 && run coldb2 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 ;;
     pin) for i in 1 2; do run pind$i 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 && run pin7_$i 300 env GOL_MULTI_VARIANT=7 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;
     cold2) run coldt 300 python -u -m pytest tests/test_gpu_engine.py -x -v --timeout 120 --timeout-method thread -k "planner or interleaved or control_word or snapshot" && for i in 1 2 3; do run coldb$i 300 env GOL_AUTOTUNE_LOG=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;

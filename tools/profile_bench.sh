@@ -1,16 +1,19 @@
 #!/bin/bash
-# Round-4 profiles that reproduce the bench line: (1) the bench exactly as the driver runs it
+# Profiles that reproduce the bench line (ROUND=r05 names the pass: gpurun_out/prof_$ROUND,
+# then tools/summarize_bench.sh writes profiles/${ROUND}_k{K}_{size}_{name}_summary.json): (1) the bench exactly as the driver runs it
 # (bench.py --gpus 1 --steps 20 --warmup 5, all configs) under --kernel-trace --stats; (2) for
 # the headline board, C3 and C2, the launch shape the bench reports (config.launch_shape /
 # configs_measured[i].launch_shape), pinned in tools/kernel_run.py (no autotune), under a
 # FETCH_SIZE pass, a WRITE_SIZE pass, a kernel trace and an SQ / GRBM pass (clock under load,
 # VALU counts) of its own -- so the traffic, the clock and the trace average of each summary
 # come from the one instantiation the bench timed.
-# tools/summarize_profile.py then writes profiles/r04_k{K}_{size}_{tag}_summary.json.
+# Since round 5 the BASELINE sizes run pinned shapes (gol_engine.cpp kKnownShapes), so the
+# shape profiled here is the shape every bench run times.
 set -u
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd /tmp && export TMPDIR=/tmp
-O="$R/gpurun_out/prof4"
+ROUND=${ROUND:-r05}
+O="$R/gpurun_out/prof_$ROUND"
 mkdir -p "$O"
 run() {  # name seconds args...
   local name=$1 t=$2; shift 2
