@@ -43,6 +43,7 @@ for step in "$@"; do
     c2sweep) run c2sweep 500 python -u tools/sweep.py --size 5120 --variants 2 --bands 16,24,32,48,64 --tpl 4,8,12,16 --mw 1 --mv 7,9,12 --turns 960 ;;
     sq65)   run sq65 300 bash tools/pmc_sq.sh ;;
     prof)   run prof 1100 bash tools/profile_bench.sh ;;
+    newr5)  run newr5 500 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_run.py -v --timeout 200 --timeout-method thread -k "pinned_shape or driver_command or harness or refuses_persistent" ;;
     fullnx) run fullnx 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
