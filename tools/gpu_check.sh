@@ -44,6 +44,7 @@ for step in "$@"; do
     sq65)   run sq65 300 bash tools/pmc_sq.sh ;;
     prof)   run prof 1100 bash tools/profile_bench.sh ;;
     newr5)  run newr5 500 python -u -m pytest tests/test_gpu_engine.py tests/test_gpu_run.py -v --timeout 200 --timeout-method thread -k "pinned_shape or driver_command or harness or refuses_persistent" ;;
+    calib5) run calib5 200 tools/calib/stencil_issue 4000 5 && (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/calib5_kt" -o run --output-format csv -- "$OLDPWD/tools/calib/stencil_issue" 4000 3 > "$OLDPWD/gpurun_out/calib5_kt.log" 2>&1 && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OLDPWD/gpurun_out/calib5_pmc" -o run --output-format csv -- "$OLDPWD/tools/calib/stencil_issue" 1000 1 > "$OLDPWD/gpurun_out/calib5_pmc.log" 2>&1); echo "calib5 prof rc=$?" ;;
     fullnx) run fullnx 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
