@@ -50,6 +50,16 @@ __device__ __forceinline__ void rsum(const uint32_t (&x)[2], uint32_t (&s)[4])
         asm("v_lshrrev_b32 %0, 1, %1" : "=v"(R) : "v"(e));
         asm("v_xor_b32 %0, %1, %2" : "=v"(wl) : "v"(L), "v"(o));
         asm("v_xor_b32 %0, %1, %2" : "=v"(er) : "v"(R), "v"(e));
+    } else if constexpr (MIX == 3) {
+        // the west funnel shift without DPP / v_alignbit: the sign bits of the odd dwords as
+        // a lane mask (one VOPC compare), shifted up one lane on the scalar unit, and added
+        // in as the carry of o + o (v_addc_co_u32, VOP3 form with the mask as carry-in):
+        // wl = (o << 1) | (west lane's o >> 31); the east shift stays DPP + v_alignbit
+        const uint64_t m = __builtin_amdgcn_ballot_w64((int)o < 0) << 1;
+        uint64_t co;
+        asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(wl), "=&s"(co) : "v"(o), "s"(m));
+        const uint32_t R = dpp_from_upper_z(e);
+        er = __builtin_amdgcn_alignbit(R, e, 1);
     } else {                                             // v_bitop3 stand-ins
         uint32_t L, R;
         asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(L) : "v"(o), "v"(e), "v"(o));
@@ -130,7 +140,8 @@ __global__ __launch_bounds__(256, (SEG <= 16 ? 8 : 6)) void k_mix(uint32_t *out,
 
 static const char *kMix[] = {"stencil (22 VALU per row: 18 v_bitop3, 2 DPP, 2 v_alignbit)",
                              "DPP / v_alignbit -> v_xor / v_lshlrev (full-rate stand-ins)",
-                             "v_bitop3 only"};
+                             "v_bitop3 only",
+                             "west shift by lane-mask carry (v_cmp + s_lshl + v_addc)"};
 
 template <int SEG, int MIX>
 static void run(int W, int turns, int ncu, int reps)
@@ -193,6 +204,7 @@ int main(int argc, char **argv)
     for (int W : {4, 6, 8}) run<16, 0>(W, turns, ncu, reps);
     for (int W : {4, 6, 8}) run<16, 1>(W, turns, ncu, reps);
     for (int W : {4, 6, 8}) run<16, 2>(W, turns, ncu, reps);
+    for (int W : {4, 6, 8}) run<16, 3>(W, turns, ncu, reps);
     for (int W : {4, 6}) run<24, 0>(W, turns, ncu, reps);
     return 0;
 }
