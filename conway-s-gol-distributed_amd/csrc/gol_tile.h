@@ -37,6 +37,13 @@
 #ifndef GOL_TILE_PAIRS_MAX   // (experiments: the longest segment that runs turns in pairs)
 #define GOL_TILE_PAIRS_MAX 12
 #endif
+// West funnel shift by lane-mask carry (one word per lane): wl = (o << 1) | (west lane's o >>
+// 31) as o + o + carry, the carry-in being the odd dwords' sign bits as a lane mask (one VOPC
+// compare) shifted up one lane on the scalar unit -- two full-rate VALU instead of a DPP move
+// and a v_alignbit, both half rate (tools/calib/stencil_issue.hip).  0 = DPP + v_alignbit.
+#ifndef GOL_TILE_WEST_CARRY
+#define GOL_TILE_WEST_CARRY 1
+#endif
 
 namespace golk {
 
@@ -140,8 +147,17 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const uint32_t e = x[2 * w], o = x[2 * w + 1];
-            const uint32_t L = dpp_from_lower_z(x[ND - 1]);   // west lane's last odd cells
-            const uint32_t wl = __builtin_amdgcn_alignbit(o, w == 0 ? L : x[2 * w - 1], 31);
+            uint32_t wl;
+            if constexpr (W == 1 && GOL_TILE_WEST_CARRY) {
+                // every lane is active here (the idle lanes run the turn too), so the mask
+                // holds every lane's sign bit; lane 0 gets carry 0, as the DPP's bound_ctrl
+                const uint64_t m = __builtin_amdgcn_ballot_w64((int)o < 0) << 1;
+                uint64_t co;
+                asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(wl), "=&s"(co) : "v"(o), "s"(m));
+            } else {
+                const uint32_t L = dpp_from_lower_z(x[ND - 1]);   // west lane's last odd cells
+                wl = __builtin_amdgcn_alignbit(o, w == 0 ? L : x[2 * w - 1], 31);
+            }
             const uint32_t er = __builtin_amdgcn_alignbit(w == W - 1 ? Rt : x[2 * w + 2], e, 1);
             s[4 * w + 0] = xor3(wl, e, o);
             s[4 * w + 1] = maj(wl, e, o);
