@@ -47,14 +47,19 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "cell updates/sec (GCUPS) at 16384² & 65536², 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 BYTES_PER_CELL_UPDATE = 0.25   # 1 bit read + 1 bit written per cell per turn
-# VALU-issue roofline of the temporal-blocking kernel (k_step_skew on the interleaved
-# layout): one stage-row of one wavefront (64 lanes x 64 cells = 4096 cell-updates) issues
-# 18 v_bitop3 (full rate: 2 SIMD cycles per wave64 instruction) + 2 v_alignbit + 2 DPP
-# moves (half rate: 4 cycles) = 52 SIMD cycles (rates: tools/calib/valu_issue.hip on
-# MI355X).  1024 SIMDs at the 2.4 GHz peak clock -> 193.6 T cell-updates/s per GPU, before
-# any redundant halo/pipeline work.
-VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES_PER_4096 = 1024, 2.4e9, 52.0
+# VALU-issue roofline of the temporal-blocking tile kernel: one row of one wavefront (64 lanes
+# x 64 cells = 4096 cell-updates) issues 22 VALU (18 v_bitop3, 2 DPP moves, 2 v_alignbit).
+# Measured ceiling (round 5, tools/calib/stencil_issue.hip, profiles/r05_stencil_issue_calib.json):
+# that exact instruction stream, in registers with no LDS / barrier / memory, all waves
+# resident, runs at 69.9 SIMD cycles per 4096 cell-updates at the production kernel's
+# segment and occupancy (SEG 24, 6 waves per SIMD; 67.8-72.0 over SEG 16/24 at 4-8 waves;
+# kernel duration x clock, confirmed by SQ_INSTS_VALU and GRBM_GUI_ACTIVE).  1024 SIMDs at the
+# 2.4 GHz peak clock -> 144.0 T cell-updates/s per GPU, before any halo or sync work.  (The
+# earlier model -- v_bitop3 at the 2-cycle wave64 floor, DPP / v_alignbit at 4: 52 cycles,
+# 193.6k -- is not reached by any measured stream: v_bitop3 alone runs 2.46-2.73 cycles.)
+VALU_SIMDS, VALU_CLOCK_HZ, VALU_CYCLES_PER_4096 = 1024, 2.4e9, 69.9
 VALU_PEAK_GCUPS = VALU_SIMDS * VALU_CLOCK_HZ / VALU_CYCLES_PER_4096 * 4096 / 1e9
+VALU_MODEL_CYCLES_PER_4096 = 52.0
 
 
 def parse():
@@ -510,9 +515,13 @@ def main():
             out["valu_roofline"] = {
                 "bound": "valu", "achieved": round(per_gpu, 1), "peak": round(VALU_PEAK_GCUPS, 1),
                 "unit": "GCUPS per GPU", "frac": round(per_gpu / VALU_PEAK_GCUPS, 4),
-                "model": "52 SIMD cycles per 4096 cell-updates (18 full-rate v_bitop3 + 4 "
-                         "half-rate v_alignbit/DPP), 1024 SIMDs x 2.4 GHz; useful cell-updates "
-                         "only (halo lanes, band halos and pipeline fill count against it)",
+                "model": "measured: the stencil's exact 22-VALU-per-row stream in registers "
+                         "(tools/calib/stencil_issue.hip, SEG 24, 6 waves per SIMD) runs 69.9 "
+                         "SIMD cycles per 4096 cell-updates; 1024 SIMDs x 2.4 GHz; useful "
+                         "cell-updates only (halo lanes, tile halos and syncs count against it)",
+                "peak_source": "profiles/r05_stencil_issue_calib.json",
+                "issue_model_peak": round(VALU_SIMDS * VALU_CLOCK_HZ / VALU_MODEL_CYCLES_PER_4096
+                                          * 4096 / 1e9, 1),
                 "clock_ghz_measured": None, "peak_at_measured_clock": None,
                 "frac_at_measured_clock": None, "clock_source": None}
             d, src = pmc_summary(W, kdepth, shape)

@@ -942,9 +942,9 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
     return pick;
 }
 
-// Pinned launch shapes for the BASELINE board sizes on an MI355X (gfx950, 256 CUs): a torus
-// engine of one of these sizes with nothing pinned by the caller runs this k_step_tile shape
-// and skips the create-time search.  The search's 0.5 ms timings put a dozen shapes within
+// Pinned launch shapes for the BASELINE board sizes on an MI355X (gfx950, 256 CUs): an engine
+// of one of these widths and buffer heights (a torus, or a row strip with its halos) with
+// nothing pinned by the caller runs this k_step_tile shape and skips the create-time search.  The search's 0.5 ms timings put a dozen shapes within
 // ~1.5 % of each other and picked different ones from box to box (round 4: 65536^2 K = 20 on
 // 336-row tiles on one box, K = 32 on 512-row tiles or k_step_skew K = 8 on others; 16384^2
 // bands 316 / 320), so the kernel a bench line timed was not reliably the one profiles/
@@ -966,11 +966,18 @@ constexpr KnownShape kKnownShapes[] = {
     {16384, 16384, {32, 316, 14, 106, 0}, 2.96f},
     // configs[1]: ORD 2, SEG 3, 16-wave workgroups; 0.57-0.59 us per turn (BENCH_r04)
     {5120, 5120, {32, 128, 14, 203, 0}, 0.58f},
+    // configs[3..4] as row strips with the bench's 128-row halos (buffer = H / N + 256 rows):
+    // N = 8 ORD 5 SEG 12 on 352-row tiles, 8 launches of 16 turns per window (5.23-5.63 us
+    // per turn against 5.61-5.71 for round 4's searched picks); N = 4 and 2 ORD 5 SEG 24 on
+    // 14 x 704 tiles (tile sweeps over the strip shapes, profiles/r05_strip_sweep.log)
+    {65536, 8448, {16, 352, 14, 512, 0}, 5.3f},
+    {65536, 16640, {32, 704, 14, 524, 0}, 9.5f},
+    {65536, 33024, {32, 704, 14, 524, 0}, 18.4f},
 };
 
 bool known_shape(const gol_ctx *c, KnownShape *out)
 {
-    if (c->ncu != 256 || is_strip(c)) return false;
+    if (c->ncu != 256) return false;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->device) != hipSuccess ||
         std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)

@@ -39,11 +39,19 @@
 #endif
 // West funnel shift by lane-mask carry (one word per lane): wl = (o << 1) | (west lane's o >>
 // 31) as o + o + carry, the carry-in being the odd dwords' sign bits as a lane mask (one VOPC
-// compare) shifted up one lane on the scalar unit -- two full-rate VALU instead of a DPP move
-// and a v_alignbit, both half rate (tools/calib/stencil_issue.hip).  0 = DPP + v_alignbit.
+// compare) shifted up one lane on the scalar unit, instead of a DPP move and a v_alignbit.
+// It issues no faster (the isolated stream: 69.4-73.5 SIMD cycles per 4096 cell-updates
+// against 67.8-70.8 for DPP + v_alignbit, tools/calib/stencil_issue.hip) but it drops the
+// DPP's data hazard (s_nop) from each row's dependency chain, which pays where the turn is
+// latency-bound: SEG 6 at 16384^2 3.02 against 3.22 us per turn, SEG 12 on the 8448-row
+// strip 5.63 against 6.06, 33024-row strip 19.2 against 21.0; SEG 24 (issue-bound, 6 waves per
+// SIMD) loses 1-3 %, SEG 3 about 1 % (profiles/r05_west_carry_ab.log).  So segments of 4..16
+// rows take it.  GOL_TILE_WEST_CARRY=0: never (A/B builds).
 #ifndef GOL_TILE_WEST_CARRY
 #define GOL_TILE_WEST_CARRY 1
 #endif
+template <int SEG, int W>
+constexpr bool tile_west_carry() { return GOL_TILE_WEST_CARRY && W == 1 && SEG >= 4 && SEG <= 16; }
 
 namespace golk {
 
@@ -148,7 +156,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         for (int w = 0; w < W; ++w) {
             const uint32_t e = x[2 * w], o = x[2 * w + 1];
             uint32_t wl;
-            if constexpr (W == 1 && GOL_TILE_WEST_CARRY) {
+            if constexpr (tile_west_carry<SEG, W>()) {
                 // every lane is active here (the idle lanes run the turn too), so the mask
                 // holds every lane's sign bit; lane 0 gets carry 0, as the DPP's bound_ctrl
                 const uint64_t m = __builtin_amdgcn_ballot_w64((int)o < 0) << 1;

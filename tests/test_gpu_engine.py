@@ -551,6 +551,8 @@ def test_driver_command_digest(gol, monkeypatch, pin):
 # width in lanes, segment code); the bench's configs run exactly these, and profiles/ has a
 # kernel-trace + PMC summary of each
 PINNED_SHAPES = {65536: (20, 336, 30, 524), 16384: (32, 316, 14, 106), 5120: (32, 128, 14, 203)}
+# ... and for 65536^2 as N row strips with 128-row halos
+PINNED_STRIP_SHAPES = {8: (16, 352, 14, 512), 4: (32, 704, 14, 524), 2: (32, 704, 14, 524)}
 
 
 @pytest.mark.parametrize("key", ["65536x65536_seed3_t1000", "16384x16384_seed2_t10000",
@@ -596,7 +598,7 @@ def test_65536_properties(gol, oracle):
 
 
 # ------------------------------------------------- full-size strip forms (C4 / C5)
-@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_65536_strips_in_process(gol, n):
     """BASELINE configs C4 / C5 in strip form at full size on one GPU: 65536^2 seed 3 as
     n row strips (the reference Server's split, Server/gol/distributor.go:106-116), each
@@ -622,6 +624,13 @@ def test_65536_strips_in_process(gol, n):
                 e.step(m)
             left -= m
         assert all(e.info().turns_per_launch > 1 for e in engs)
+        # the strips run their pinned MI355X shape (gol_engine.cpp kKnownShapes), the shape the
+        # N-GPU bench times on every rank
+        K_, th, tw, code = PINNED_STRIP_SHAPES[n]
+        for e in engs:
+            i = e.info()
+            assert (i.shape_source, i.turns_per_launch, i.band_rows) == (2, K_, th), n
+            assert {(t[0], t[1]) for t in e.last_launch_tiles(blocks=True)} == {(tw, code)}
         assert sum(e.snapshot()[1] for e in engs) == d["alive"]
         hs = hashlib.sha256()
         for e in engs:
