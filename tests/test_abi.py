@@ -144,3 +144,25 @@ def test_product_does_not_import_oracle():
                 text = open(os.path.join(dp, f)).read()
                 for b in bad:
                     assert b not in text, (f, b)
+
+
+def test_pinned_shapes_match_the_tests():
+    """The pinned MI355X launch shapes (gol_engine.cpp kKnownShapes) are the ones the GPU
+    digests assert (test_gpu_engine.py PINNED_SHAPES / PINNED_STRIP_SHAPES), every code is a
+    shipped instantiation, and profile_bench.sh can profile them (read from the source: no
+    device needed)."""
+    import re
+    from conftest import TILE_CODES
+    from gol import _native as N
+    src = open(os.path.join(os.path.dirname(os.path.dirname(N.LIB_PATH)), "csrc",
+                            "gol_engine.cpp")).read()
+    body = src[src.index("constexpr KnownShape kKnownShapes[] = {"):]
+    body = body[:body.index("};")]
+    got = {(int(w), int(r)): (int(k), int(th), int(tw), int(code)) for w, r, k, th, tw, code in
+           re.findall(r"\{(\d+), (\d+), \{(\d+), (\d+), (\d+), (\d+), 0\}", body)}
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import test_gpu_engine as T
+    want = {(s, s): v for s, v in T.PINNED_SHAPES.items()}
+    want.update({(65536, 65536 // n + 256): v for n, v in T.PINNED_STRIP_SHAPES.items()})
+    assert got == want
+    assert all(v[3] in TILE_CODES for v in got.values())
