@@ -991,6 +991,63 @@ bool known_shape(const gol_ctx *c, KnownShape *out)
     return false;
 }
 
+// A pinned shape is checked on the engine's own buffers before it is used: synchronised
+// launches of its depth, the way gol_step runs them, for ~GOL_PIN_VERIFY_MS (default 60) ms;
+// when the median time per turn is more than 1.35x the table's figure -- a device unlike the
+// one the table was measured on -- the engine runs the search instead.  (Like the search did,
+// this keeps the GPU busy right before the caller's first steps: an MI355X that idled drops
+// its clock, and a 20-turn 65536^2 call then takes 810-850 us instead of 700,
+// profiles/r04_clock_ramp_20turn.log, profiles/r05_prewarm_probe.log.)
+bool verify_pinned(gol_ctx *c, const KnownShape &ks)
+{
+    const char *v = getenv("GOL_PIN_VERIFY_MS");
+    const double budget_ms = v ? atof(v) : 60.0;
+    if (budget_ms <= 0) return true;
+    golk::StepArgs a{};
+    a.width = c->cfg.width;
+    a.nw = c->nw;
+    a.pitch = c->pitch;
+    a.modrows = c->buf_rows;
+    a.row_lo = 0;
+    a.row_hi = c->buf_rows;
+    a.multi_words = 1;
+    a.multi_variant = golk::kMultiTile;
+    a.err = c->d_err;
+    a.band = ks.t.th;
+    a.tile_w = ks.t.tw;
+    a.tile_seg = ks.t.seg;
+    if (golk::launch_fill_random(c->board[0], c->cfg.width, c->nw, c->pitch, c->buf_rows, 0,
+                                 c->buf_rows, 12345, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return false;
+    // bursts of ~1 ms of launches, each ended by a sync (host wall time, as gol_step runs)
+    const int n = std::max(1, (int)std::ceil(1000.0 / (ks.t.K * ks.us_per_turn)));
+    std::vector<float> us;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < 2000; ++i) {
+        const auto s0 = std::chrono::steady_clock::now();
+        for (int j = 0; j < n; ++j) {
+            a.in = c->board[j & 1];
+            a.out = c->board[(j + 1) & 1];
+            if (golk::launch_step_multi(a, ks.t.K, c->stream) != hipSuccess) return false;
+        }
+        if (hipStreamSynchronize(c->stream) != hipSuccess) return false;
+        const auto s1 = std::chrono::steady_clock::now();
+        us.push_back(std::chrono::duration<float, std::micro>(s1 - s0).count() / (n * ks.t.K));
+        if (std::chrono::duration<double, std::milli>(s1 - t0).count() >= budget_ms && i >= 8) break;
+    }
+    (void)hipGetLastError();
+    if (check_dev_err(c) != GOL_OK) return false;
+    std::vector<float> tail(us.begin() + us.size() / 2, us.end());
+    std::sort(tail.begin(), tail.end());
+    const float med = tail[tail.size() / 2];
+    if (getenv("GOL_AUTOTUNE_LOG"))
+        fprintf(stderr, "pinned shape %dx%d K=%d tile=%dx%d code=%d: %zu launches, median %.3f us per "
+                "turn (table %.3f)\n", c->cfg.width, c->buf_rows, ks.t.K, ks.t.tw, ks.t.th, ks.t.seg,
+                us.size(), med, ks.us_per_turn);
+    return med <= 1.35f * ks.us_per_turn;
+}
+
 // Boards below 2^20 words (5120^2: 409 600) cannot fill the GPU with band pipelines: they run
 // k_step_tile at the measured-best shape.
 // K1p for a small torus board at the tuned tile shape: 256 turns as one k_tile_persist launch
@@ -1756,7 +1813,7 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     // a BASELINE board size on an MI355X: the pinned shape, no search (GOL_AUTOTUNE=2: search)
     KnownShape ks{};
     if (tuning && !pinned && cfg->turns_per_launch <= 0 && !getenv("GOL_TILE") &&
-        !(at && atoi(at) == 2) && known_shape(c, &ks)) {
+        !(at && atoi(at) == 2) && known_shape(c, &ks) && verify_pinned(c, ks)) {
         apply_tile(c, ks.t);
         c->tuned_us_per_turn = ks.us_per_turn;
         c->shape_source = 2;

@@ -10,6 +10,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "conway-s-gol-distributed_amd"))
+os.environ["GOL_PIN_VERIFY_MS"] = "0"     # (the engine's own pre-load is what X stands in for)
 import torch  # noqa: E402
 
 import gol  # noqa: E402
