@@ -853,7 +853,7 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         // cycles per instruction against 2.43 at 4 waves); 30 x 536 tiles of SEG 24 ran 34.6
         // us per turn at 65536^2 against 36.3 for the best 4-wave shape
         // (profiles/r04_sweep_65536_ord5.log)
-        static constexpr int kSix[] = {524, 624, 516, 616};
+        static constexpr int kSix[] = {524, 724, 624, 516, 616};
         static_assert(all_shipped(kSix), "a tile code outside kTileCodes");
         for (int sg : kSix)
             for (int tw : {tws.empty() ? 30 : tws[0], 14})

@@ -68,7 +68,8 @@ constexpr size_t tile_lds_bytes(int threads, int words)
 // 4: ORD 1 with no workgroup barrier -- each wave waits only for its two neighbour waves'
 // published edge sums, through per-wave progress flags in LDS; 5: ORD 1 with the edge sums
 // read back from LDS instead of kept in registers; 6: ORD 5 with the barrier after the
-// interior rows), words per lane
+// interior rows; 7: ORD 5 with the tile's two halo segments in wave 0, which skips the rows
+// the shrinking trapezoid no longer needs -- see tile_pass), words per lane
 constexpr int tile_seg_rows(int code) { return code % 100; }
 constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
 
@@ -104,8 +105,19 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int group = lane / C, col = lane - group * C;
     const bool live = group < G;                         // lanes past G groups: idle
-    const int seg = wave * G + group;                    // segment index within the tile
     const int nseg = (TH + 2 * K + SEG - 1) / SEG;       // segments the tile needs
+    // ORD 7 (G == 2, nseg >= 3; host-checked): wave 0 holds the top segment (group 0) and the
+    // bottom one (group 1, its rows in reverse order), the other waves the segments between,
+    // in order.  Both of wave 0's segments then leave the trapezoid from their local row 0
+    // on: turn t changes tile rows [t + 1, 2K + TH - 1 - t), so local rows 0 .. t of either
+    // segment are outside it, and wave 0 can skip them for both groups at once (turn4 below).
+    // The rule is symmetric in up and down, so a reversed segment runs the same body; only
+    // its loads, stores and LDS edge slots are mirrored.
+    constexpr bool kHalo = ORD == 7;
+    static_assert(!kHalo || W == 1, "ORD 7: one word per lane");
+    const int seg = !kHalo ? wave * G + group
+                           : wave == 0 ? (group == 0 ? 0 : nseg - 1) : (wave - 1) * G + group + 1;
+    const bool rev = kHalo && wave == 0 && group == 1;   // (a lane-varying flag: group 1 only)
     const int slot = seg * C + col;
 
     // lane column (torus wrap) and the lane's rows: tile row t = seg * SEG + i is buffer row
@@ -116,10 +128,11 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     const int M = a.modrows;
     const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
     const uint32_t span = (uint32_t)M * pitch_b;
-    int r = y0 - K + (live ? seg : 0) * SEG;
+    int r = y0 - K + (live ? seg : 0) * SEG + (rev ? SEG - 1 : 0);
     while (r < 0) r += M;
     while (r >= M) r -= M;
     uint32_t off = (uint32_t)r * pitch_b + (uint32_t)gx * (8u * W);
+    const uint32_t lstep = rev ? span - pitch_b : pitch_b;   // (a reversed segment loads upwards)
     const __amdgpu_buffer_rsrc_t rin =
         __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)span, kBufFlags);
     const __amdgpu_buffer_rsrc_t rout =
@@ -143,7 +156,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             v[i][2] = w.z;
             v[i][3] = w.w;
         }
-        off += pitch_b;
+        off += lstep;
         off = off >= span ? off - span : off;            // (the column stays < pitch_b)
     }
 
@@ -209,6 +222,12 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     const int myslot = live ? slot : nlive + wave * (64 - G * C) + (lane - G * C);
     const int s_up = live && seg > 0 ? slot - C : myslot;
     const int s_dn = live && seg + 1 < nseg ? slot + C : myslot;
+    // a lane's own edge slots and its neighbours', by the lane's local row order: its first
+    // row's sums go to the top-edge array and its last row's to the bottom-edge array, and it
+    // reads the bottom edge of the segment above and the top edge of the one below -- all
+    // mirrored for a reversed segment (ORD 7), whose first row is physically its bottom one
+    const int o_wt = (rev ? (int)nslot : 0) + myslot, o_wb = (rev ? 0 : (int)nslot) + myslot;
+    const int o_up = rev ? s_dn : (int)nslot + s_up, o_dn = rev ? (int)nslot + s_up : s_dn;
     // Turn parity p uses the slots 2 p nslot further on.  Short segments run two turns per
     // loop iteration with p a compile-time constant (the parity's addresses hoisted out of the
     // loop: 11 % faster turns at SEG 3-4); long ones one turn body with the offset added per
@@ -218,22 +237,23 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     constexpr bool kPairs = SEG * W <= GOL_TILE_PAIRS_MAX;
     // (with pairs the lane's four LDS addresses of each parity are loop-invariant registers;
     // one body forms them per turn -- precomputed there, the long bodies ran 4-8 % slower)
-    uint4 *const wtop2[2] = {xsh + myslot, xsh + 2 * nslot + myslot};
-    uint4 *const wbot2[2] = {xsh + nslot + myslot, xsh + 3 * nslot + myslot};
-    const uint4 *const rup2[2] = {xsh + nslot + s_up, xsh + 3 * nslot + s_up};
-    const uint4 *const rdn2[2] = {xsh + s_dn, xsh + 2 * nslot + s_dn};
-    auto wtop = [&](int p, int off) { return kPairs ? wtop2[p] : xsh + off + myslot; };
-    auto wbot = [&](int p, int off) { return kPairs ? wbot2[p] : xsh + off + nslot + myslot; };
-    auto rup = [&](int p, int off) {
-        return kPairs ? rup2[p] : (const uint4 *)(xsh + off + nslot + s_up);
-    };
-    auto rdn = [&](int p, int off) { return kPairs ? rdn2[p] : (const uint4 *)(xsh + off + s_dn); };
+    uint4 *const wtop2[2] = {xsh + o_wt, xsh + 2 * nslot + o_wt};
+    uint4 *const wbot2[2] = {xsh + o_wb, xsh + 2 * nslot + o_wb};
+    const uint4 *const rup2[2] = {xsh + o_up, xsh + 2 * nslot + o_up};
+    const uint4 *const rdn2[2] = {xsh + o_dn, xsh + 2 * nslot + o_dn};
+    auto wtop = [&](int p, int off) { return kPairs ? wtop2[p] : xsh + off + o_wt; };
+    auto wbot = [&](int p, int off) { return kPairs ? wbot2[p] : xsh + off + o_wb; };
+    auto rup = [&](int p, int off) { return kPairs ? rup2[p] : (const uint4 *)(xsh + off + o_up); };
+    auto rdn = [&](int p, int off) { return kPairs ? rdn2[p] : (const uint4 *)(xsh + off + o_dn); };
     // A wave whose rows are all outside the turn's trapezoid leaves: the tile's rows
     // [t + 1, 2K + TH - 1 - t) change at turn t (t = 0 .. K-1) and need the sums of the rows
     // one further out; a wave above row t (below row 2K + TH - 1 - t) holds no row that any
     // later turn or the final store needs (its rows are < K, resp. >= K + TH), and the
     // workgroup barrier no longer counts it once it has ended.
-    const int wrow0 = wave * G * SEG, wrow1 = wrow0 + G * SEG;  // the wave's tile rows
+    // the wave's tile rows (ORD 7: wave 0 spans the whole tile -- it never leaves; wave w > 0
+    // holds segments (w - 1) G + 1 ..)
+    const int wrow0 = !kHalo ? wave * G * SEG : wave == 0 ? 0 : ((wave - 1) * G + 1) * SEG;
+    const int wrow1 = !kHalo ? wrow0 + G * SEG : wave == 0 ? 1 << 30 : wrow0 + G * SEG;
     // ORD 4: per-wave progress flags after the slot arrays.  flag[w] = the last turn whose
     // edge sums wave w has published (-1 before the first; INT_MAX once it has left), written
     // by lane 0 after its sums: the LDS serves one wave's requests in issue order, so a wave
@@ -272,8 +292,16 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     // occupancy sweep).  ORD 6: the barrier where ORD 4 waits, after the interior rows (ORD
     // 2's placement: a wave that arrives early has done all the work that needs no neighbour;
     // the turn-parity double buffer still needs only the one barrier per turn)
-    auto turn4 = [&](auto P, int poff, int t) {
+    // ORD 7's wave 0 skips, at turn t, its rows lo = t + 1 (at most SEG - 2) and above only:
+    // local rows 0 .. t of both its segments are outside the trapezoid.  Rows below lo - 1 are
+    // neither summed nor updated, row lo - 1 is summed (the neighbour of row lo), and row 0's
+    // rule and its neighbour read go too; each skip is a wave-uniform scalar branch (the other
+    // waves pass lo = 0 and never take one).  A skipped row goes stale exactly when the
+    // trapezoid makes it junk, and row lo reads only rows lo - 1 .., which were updated at turn
+    // t - 1 (their lo was t).  For every other turn order lo is the constant 0.
+    auto turn4 = [&](auto P, int poff, int t, int lo_rt) {
         constexpr int p = decltype(P)::value;
+        const int lo = ORD == 7 ? lo_rt : 0;
         const int off = poff;
         uint32_t Pw[NS], Q[NS], S1[NS];
         {
@@ -282,20 +310,20 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             rsum(v[SEG - 1], Lr);
             put(wtop(p, off), F);
             put(wbot(p, off), Lr);
-            if constexpr (ORD == 5) __syncthreads();
+            if constexpr (ORD == 5 || ORD == 7) __syncthreads();
             else if constexpr (ORD == 4) publish(t);
 #pragma unroll
             for (int k = 0; k < NS; ++k) Pw[k] = F[k];
         }
-        rsum(v[1], Q);
+        if (lo <= 2) rsum(v[1], Q);
 #pragma unroll
         for (int k = 0; k < NS; ++k) S1[k] = Q[k];
 #pragma unroll
         for (int i = 1; i + 1 < SEG; ++i) {
             uint32_t R[NS];
             if (i + 2 == SEG) get(wbot(p, off), R);   // (own bottom slot: Lr)
-            else rsum(v[i + 1], R);
-            rule(Pw, Q, R, v[i]);
+            else if (i + 2 >= lo) rsum(v[i + 1], R);
+            if (i >= lo) rule(Pw, Q, R, v[i]);
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
                 Pw[k] = Q[k];
@@ -311,16 +339,18 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         if constexpr (ORD == 6) __syncthreads();
         else await_neighbours(t);
         uint32_t U[NS], D[NS], F[NS];
-        get(rup(p, off), U);
-        get(wtop(p, off), F);
-        rule(U, F, S1, v[0]);
+        if (lo == 0) {
+            get(rup(p, off), U);
+            get(wtop(p, off), F);
+            rule(U, F, S1, v[0]);
+        }
         get(rdn(p, off), D);
         get(wbot(p, off), F);                                 // (Lr)
         rule(Pw, F, D, v[SEG - 1]);
     };
     auto turn = [&](auto P, int poff, int t) {
         if constexpr (ORD >= 4) {
-            turn4(P, poff, t);
+            turn4(P, poff, t, kHalo && wave == 0 ? min(t + 1, SEG - 2) : 0);
             return;
         }
         constexpr int p = decltype(P)::value;
@@ -417,7 +447,18 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         }
     };
     bool gone = false;
-    if constexpr (!kPairs) {
+    if constexpr (kHalo) {
+        static_assert(!kPairs, "ORD 7: long segments");
+        for (int t = 0; t < K; ++t) {
+            // (wave 0 spans the whole tile and never leaves: wrow1 is out of reach)
+            if (!PERSIST && (wrow1 <= t || wrow0 > lastrow - t)) {   // (wave-uniform)
+                leave(t);
+                gone = true;
+                break;
+            }
+            turn(std::integral_constant<int, 0>{}, (t & 1) * 2 * nslot, t);
+        }
+    } else if constexpr (!kPairs) {
         for (int t = 0; t < K; ++t) {
             if (!PERSIST && (wrow1 <= t || wrow0 > lastrow - t)) {   // (wave-uniform)
                 leave(t);
@@ -446,16 +487,18 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     if (!PERSIST && gone) return;
     // interior rows [K, K + TH) of the tile, below row_hi; interior columns inside the row
     if (gone || !live || col < 1 || col > TW || x0 + col - 1 >= nl) return;
-    const int t0 = seg * SEG;
+    const int t0 = seg * SEG + (rev ? SEG - 1 : 0);
+    const int dr = rev ? -1 : 1;
+    const uint32_t sstep = rev ? 0u - pitch_b : pitch_b;
     // per-lane byte offset (the segment differs between the lane groups of a wave); rows
     // y0 - K + t0 + i are stored only once inside [row_lo, row_hi): no wrap, and the
     // unsigned sum is exact there even if the first row of the segment lies above row 0
     uint32_t so = (uint32_t)(y0 - K + t0) * pitch_b + (uint32_t)(x0 + col - 1) * (8u * W);
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
-        const int tr = t0 + i;
+        const int tr = t0 + dr * i;
         if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) buf_store(v[i], rout, so, 0);
-        so += pitch_b;
+        so += sstep;
     }
 }
 
@@ -469,7 +512,7 @@ __device__ __forceinline__ int tile_of_block(int ntiles)
 
 // (ORD 4 up to SEG 16: 64 VGPRs, 8 waves per SIMD -- two 16-wave workgroups per CU)
 template <int SEG, int ORD, int W>
-__global__ __launch_bounds__(1024, 1) void k_step_tile(const uint64_t *__restrict__ in,
+__global__ __launch_bounds__(1024, (ORD == 7 ? 6 : 1)) void k_step_tile(const uint64_t *__restrict__ in,
                                                      uint64_t *__restrict__ out, StepArgs a,
                                                      int turns, int ntx, int ntiles)
 {

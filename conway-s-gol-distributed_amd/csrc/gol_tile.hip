@@ -115,6 +115,9 @@ void *tile_kernel(int code)
     if (ord == 4) return w == 1 && seg >= 3 && seg <= 40 ? tile_fn<4, 1>(seg) : nullptr;
     if (ord == 5) return w == 1 && seg >= 3 && seg <= 40 ? tile_fn<5, 1>(seg) : nullptr;
     if (ord == 6) return w == 1 ? tile_fn6(seg) : nullptr;
+    // ORD 7 (wave 0 holds the halo segments and skips the rows the trapezoid has left): the
+    // 65536^2 segment only
+    if (ord == 7) return w == 1 && seg == 24 ? reinterpret_cast<void *>(&k_step_tile<24, 7, 1>) : nullptr;
     if (ord > 2) return nullptr;
     if (w == 2) return ord == 2 ? tile_fn<2, 2>(seg) : ord ? tile_fn<1, 2>(seg) : tile_fn<0, 2>(seg);
     return ord == 2 ? tile_fn<2, 1>(seg) : ord ? tile_fn<1, 1>(seg) : tile_fn<0, 1>(seg);
@@ -127,8 +130,11 @@ bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
     if (!GOL_TOOLS && !tile_code_shipped(seg)) return false;   // (untested instantiations)
     if (nw % tile_seg_words(seg)) return false;          // (whole word pairs per lane)
     const int C = tile_w + 2, G = 64 / C;
+    const int ord = seg / 100 % 10;
     seg %= 100;
     const int nseg = (tile_h + 2 * turns + seg - 1) / seg;
+    // ORD 7: two lane groups per wave (wave 0 = the top and the bottom segment), >= 3 segments
+    if (ord == 7 && (G != 2 || nseg < 3)) return false;
     return (nseg + G - 1) / G <= kTileMaxWaves;
 }
 

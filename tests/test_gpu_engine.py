@@ -547,6 +547,27 @@ def test_driver_command_digest(gol, monkeypatch, pin):
         assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
 
 
+@pytest.mark.parametrize("K,key", [(20, "65536x65536_seed3_t25"), (24, "65536x65536_seed3_t1000")])
+def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key):
+    """ORD 7 (code 724: wave 0 holds the tile's top segment and its bottom segment in reverse
+    row order, and skips the rows the shrinking trapezoid has left) on 30 x 336 tiles at full
+    size against the oracle digests: K = 20 (the bottom segment reaches 8 rows past the
+    loaded halo) and K = 24 (both segments are exactly the 24 halo rows)."""
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+    monkeypatch.setenv("GOL_TILE", "30,724")
+    d = _digests()[key]
+    with _engine(gol, d["width"], d["height"], band_rows=336, turns_per_launch=K) as e:
+        e.fill_random(d["seed"])
+        if d["turns"] == 25:
+            e.step(5)
+            e.step(20)
+        else:
+            e.step(d["turns"])
+        assert {(t[0], t[1]) for t in e.last_launch_tiles()} == {(30, 724)}
+        assert e.snapshot() == (d["turns"], d["alive"])
+        assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
+
+
 # the pinned MI355X launch shapes (gol_engine.cpp kKnownShapes): board -> (K, tile height, tile
 # width in lanes, segment code); the bench's configs run exactly these, and profiles/ has a
 # kernel-trace + PMC summary of each
