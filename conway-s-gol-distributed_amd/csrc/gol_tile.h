@@ -292,13 +292,15 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     // occupancy sweep).  ORD 6: the barrier where ORD 4 waits, after the interior rows (ORD
     // 2's placement: a wave that arrives early has done all the work that needs no neighbour;
     // the turn-parity double buffer still needs only the one barrier per turn)
-    // ORD 7's wave 0 skips, at turn t, its rows lo = t + 1 (at most SEG - 2) and above only:
-    // local rows 0 .. t of both its segments are outside the trapezoid.  Rows below lo - 1 are
-    // neither summed nor updated, row lo - 1 is summed (the neighbour of row lo), and row 0's
-    // rule and its neighbour read go too; each skip is a wave-uniform scalar branch (the other
-    // waves pass lo = 0 and never take one).  A skipped row goes stale exactly when the
-    // trapezoid makes it junk, and row lo reads only rows lo - 1 .., which were updated at turn
-    // t - 1 (their lo was t).  For every other turn order lo is the constant 0.
+    // ORD 7's wave 0 updates, at turn t, only its rows lo = t + 1 (at most SEG - 2) and above:
+    // local rows 0 .. t of both its segments are outside the trapezoid.  The rules of the rows
+    // below lo (14 of a row's 22 VALU) and row 0's neighbour read are skipped by wave-uniform
+    // scalar branches (the other waves pass lo = 0 and never take one); the row sums stay
+    // unconditional -- skipping them too made the sliding window's values conditional, and
+    // the compiler paid 4 v_mov per row on every wave's path to merge them.  A skipped row goes
+    // stale exactly when the trapezoid makes it junk, and row lo reads only rows lo - 1 ..,
+    // which were updated at turn t - 1 (their lo was t).  For every other turn order lo is the
+    // constant 0.
     auto turn4 = [&](auto P, int poff, int t, int lo_rt) {
         constexpr int p = decltype(P)::value;
         const int lo = ORD == 7 ? lo_rt : 0;
@@ -315,14 +317,14 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
 #pragma unroll
             for (int k = 0; k < NS; ++k) Pw[k] = F[k];
         }
-        if (lo <= 2) rsum(v[1], Q);
+        rsum(v[1], Q);
 #pragma unroll
         for (int k = 0; k < NS; ++k) S1[k] = Q[k];
 #pragma unroll
         for (int i = 1; i + 1 < SEG; ++i) {
             uint32_t R[NS];
             if (i + 2 == SEG) get(wbot(p, off), R);   // (own bottom slot: Lr)
-            else if (i + 2 >= lo) rsum(v[i + 1], R);
+            else rsum(v[i + 1], R);
             if (i >= lo) rule(Pw, Q, R, v[i]);
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
