@@ -853,7 +853,7 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         // cycles per instruction against 2.43 at 4 waves); 30 x 536 tiles of SEG 24 ran 34.6
         // us per turn at 65536^2 against 36.3 for the best 4-wave shape
         // (profiles/r04_sweep_65536_ord5.log)
-        static constexpr int kSix[] = {524, 724, 624, 516, 616};
+        static constexpr int kSix[] = {524, 624, 516, 616};
         static_assert(all_shipped(kSix), "a tile code outside kTileCodes");
         for (int sg : kSix)
             for (int tw : {tws.empty() ? 30 : tws[0], 14})
@@ -957,10 +957,10 @@ struct KnownShape {
     float us_per_turn;                       // measured steady state (round-4 sweeps)
 };
 constexpr KnownShape kKnownShapes[] = {
-    // configs[3..4]: ORD 5, SEG 24, 8-wave workgroups (6 waves per SIMD); 34.5-34.7 us per turn
-    // (profiles/r04_sweep_65536_ord5.log, r04_sweep_65536_fine.log); the driver's 20-turn call
-    // is one launch of this shape
-    {65536, 65536, {20, 336, 30, 524, 0}, 34.6f},
+    // configs[3..4]: ORD 5, SEG 24, 8-wave workgroups (6 waves per SIMD); 34.0-34.7 us per turn
+    // (profiles/r04_sweep_65536_ord5.log, r04_sweep_65536_fine.log; K = 24 ~1 % ahead of K = 20,
+    // profiles/r05_ord7_ab.log); the driver's 20-turn call is one 20-turn launch of this shape
+    {65536, 65536, {24, 336, 30, 524, 0}, 34.0f},
     // configs[2]: ORD 1, SEG 6, 16-wave workgroups (8 waves per SIMD), two residency rounds;
     // 2.94-3.02 us per turn (BENCH_r04 configs_measured)
     {16384, 16384, {32, 316, 14, 106, 0}, 2.96f},

@@ -206,7 +206,6 @@ constexpr int kTileCodes[] = {
     403,  404,  406,  408,  412,  416,  424,  432,  440,                        // ORD 4
     503,  504,  506,  508,  512,  516,  524,  532,  540,                        // ORD 5
     612,  616,  624,                                                            // ORD 6
-    724,                                                                        // ORD 7
     1002, 1003, 1004, 1006, 1008,                                               // W 2
     1102, 1103, 1104, 1106, 1108,
     1204, 1206, 1208,

@@ -27,7 +27,6 @@ TILE_CODES = (2, 3, 4, 6, 8, 12, 16, 24, 32, 40, 48,
               403, 404, 406, 408, 412, 416, 424, 432, 440,
               503, 504, 506, 508, 512, 516, 524, 532, 540,
               612, 616, 624,
-              724,
               1002, 1003, 1004, 1006, 1008,
               1102, 1103, 1104, 1106, 1108,
               1204, 1206, 1208)

@@ -547,6 +547,7 @@ def test_driver_command_digest(gol, monkeypatch, pin):
         assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
 
 
+@tools_only
 @pytest.mark.parametrize("K,key", [(20, "65536x65536_seed3_t25"), (24, "65536x65536_seed3_t1000")])
 def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key):
     """ORD 7 (code 724: wave 0 holds the tile's top segment and its bottom segment in reverse
@@ -571,7 +572,7 @@ def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key):
 # the pinned MI355X launch shapes (gol_engine.cpp kKnownShapes): board -> (K, tile height, tile
 # width in lanes, segment code); the bench's configs run exactly these, and profiles/ has a
 # kernel-trace + PMC summary of each
-PINNED_SHAPES = {65536: (20, 336, 30, 524), 16384: (32, 316, 14, 106), 5120: (32, 128, 14, 203)}
+PINNED_SHAPES = {65536: (24, 336, 30, 524), 16384: (32, 316, 14, 106), 5120: (32, 128, 14, 203)}
 # ... and for 65536^2 as N row strips with 128-row halos
 PINNED_STRIP_SHAPES = {8: (16, 352, 14, 512), 4: (32, 704, 14, 524), 2: (32, 704, 14, 524)}
 
@@ -770,7 +771,7 @@ def _pinned_shape(code):
     return (14, 100) if seg <= 8 else (30, 100)   # 66 words = 4 x 14 + 10 = 2 x 30 + 6
 
 
-@pytest.mark.parametrize("code", TILE_CODES)
+@pytest.mark.parametrize("code", list(TILE_CODES) + _tools(724))
 def test_tile_code_pinned(gol, oracle, monkeypatch, code):
     """Every k_step_tile instantiation the product library can run (gol_tile_codes; the shape
     searches pick only these) against the oracle: ragged tiles in both directions, one launch
@@ -905,7 +906,7 @@ def test_tile_codes_outside_the_list_rejected(gol, monkeypatch):
     if os.environ.get("GOL_AMD_LIB", "").endswith("_tools.so"):
         pytest.skip("tools build accepts them")
     from gol import _native as N
-    for code in (5, 148, 302, 1012):
+    for code in (5, 148, 302, 1012, 724):
         monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
         monkeypatch.setenv("GOL_TILE", f"14,{code}")
         with pytest.raises(N.GolError) as ei:
