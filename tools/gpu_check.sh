@@ -53,7 +53,8 @@ for step in "$@"; do
     wide65) run wide65 500 python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:20,30:344:524:20,62:472:532:20,62:448:532:32,62:344:524:20,62:456:532:24,62:472:132:20,62:608:540:16,62:600:540:20,30:536:524:20,14:720:524:24 ;;
     prewarm) run prewarm 300 python -u tools/prewarm_probe.py 0,10,30,60,100,300 && for i in 1 2 3; do run b20v$i 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; run b20nv$i 200 env GOL_PIN_VERIFY_MS=0 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;
     ord7)   run ord7t 300 python -u -m pytest tests/test_gpu_engine.py -v --timeout 200 --timeout-method thread -k "halo_wave or test_tile_code_pinned" && run ord7ab 400 python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:20,30:336:724:20,30:336:724:24,30:344:724:20,30:336:524:24,14:720:524:24 && run ord7ab2 400 python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:724:20,30:336:524:20,30:336:724:24,30:336:524:24 ;;
-    retune) run retune16 400 env GOL_AUTOTUNE=2 GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 16384 --auto --turns 640 --rounds 3 --shapes 14:316:106:32,14:320:108:32,14:316:206:32,14:320:112:32,14:352:512:16,14:316:506:32,30:320:108:32,14:448:108:32,14:456:112:24 && run retune5 300 env GOL_AUTOTUNE=2 GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --rounds 3 --shapes 14:128:203:32,14:128:104:32,14:128:204:32,14:128:106:32,10:160:104:32,14:128:504:32,14:160:104:32 ;;
+    retune16) run retune16 400 env GOL_AUTOTUNE=2 GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 16384 --auto --turns 640 --rounds 3 --shapes 14:316:106:32,14:320:108:32,14:316:206:32,14:320:112:32,14:352:512:16,14:316:506:32,30:320:512:32,30:320:112:32,30:320:516:32,30:352:516:16,14:448:108:32,14:456:112:24 ;;
+    retune5) run retune5 300 env GOL_AUTOTUNE=2 GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --rounds 3 --shapes 14:128:203:32,14:128:104:32,14:128:204:32,14:128:106:32,10:160:104:32,14:128:504:32,14:160:104:32 ;;
     fullnx) run fullnx 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
