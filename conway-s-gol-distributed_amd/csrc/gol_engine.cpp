@@ -921,6 +921,11 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
         std::sort(top.begin(), top.end(),
                   [](const auto &x, const auto &y) { return x.first < y.first; });
         if (top.size() > 4) top.resize(4);
+        // ... and among the shapes within 1 % of the fastest of that round (timing noise from
+        // box to box), a fixed order decides -- the deepest K, then the lowest segment code,
+        // the widest tile, the tallest -- so two boxes that time the same shapes within noise
+        // pick the same one
+        std::vector<std::pair<float, TileShape>> fin;
         float fbest = 0.f;
         for (const auto &c2 : top) {
             float v = 0.f;
@@ -928,12 +933,21 @@ TileShape tile_search(gol_ctx *c, int kfix, float *us, int W)
                 const float u = time_one(c2.second, reps);
                 if (u > 0.f && (v == 0.f || u < v)) v = u;
             }
-            if (v > 0.f && (fbest == 0.f || v < fbest)) {
-                fbest = v;
-                pick = c2.second;
+            if (v > 0.f) {
+                fin.push_back({v, c2.second});
+                if (fbest == 0.f || v < fbest) fbest = v;
             }
         }
-        if (fbest > 0.f) best = fbest;
+        auto before = [](const TileShape &x, const TileShape &y) {
+            return std::make_tuple(-x.K, x.seg, -x.tw, -x.th) < std::make_tuple(-y.K, y.seg, -y.tw, -y.th);
+        };
+        bool have = false;
+        for (const auto &f : fin)
+            if (f.first <= 1.01f * fbest && (!have || before(f.second, pick))) {
+                pick = f.second;
+                best = f.first;
+                have = true;
+            }
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
