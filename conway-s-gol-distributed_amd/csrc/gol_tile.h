@@ -31,6 +31,7 @@
 // SEG and K.
 #pragma once
 #include "gol_device.h"
+#include "gol_tile_turn.h"
 
 #include <type_traits>
 
@@ -47,6 +48,12 @@
 // strip 5.63 against 6.06, 33024-row strip 19.2 against 21.0; SEG 24 (issue-bound, 6 waves per
 // SIMD) loses 1-3 %, SEG 3 about 1 % (profiles/r05_west_carry_ab.log).  So segments of 4..16
 // rows take it.  GOL_TILE_WEST_CARRY=0: never (A/B builds).
+// K1t ORD 8 / 9 (the turn in inline asm, gol_tile_turn.h): bit 1 = the workgroup barrier after
+// rows 1 and 2 instead of right after the edge sums' stores, bit 2 = LDS slots 16 B apart
+// instead of 64 (A/B builds: make variant VDEFS=-DGOL_TURN_VAR=n)
+#ifndef GOL_TURN_VAR
+#define GOL_TURN_VAR 0
+#endif
 #ifndef GOL_TILE_WEST_CARRY
 #define GOL_TILE_WEST_CARRY 1
 #endif
@@ -449,7 +456,68 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         }
     };
     bool gone = false;
-    if constexpr (kHalo) {
+    if constexpr (ORD == 8 || ORD == 9) {
+        // ORD 8: ORD 5's turn as one inline-asm block with a hand-made VGPR assignment
+        // (gol_tile_turn.h, generated by gen_tile_turn.py: every v_bitop3 reads registers of
+        // both parities, which the compiler's allocation does not ensure -- a v_bitop3 whose
+        // sources all have one parity issues at half rate).  LDS: 64 B per slot, [slot][top,
+        // bottom][turn parity]; the asm toggles the parity (bit 4) of the three addresses.
+        // ORD 9: the same with the lane shifts' neighbour words fetched by ds_bpermute_b32 (the
+        // LDS pipe) one row ahead instead of DPP moves (half-rate VALU instructions); lane l
+        // reads lane l - 1 at address ba and lane l + 1 at ba + 8 (the wrap reaches only halo
+        // and idle lanes, whose cells are junk anyway)
+        static_assert(W == 1 && !PERSIST && SEG % 3 == 0, "ORD 8/9: one word per lane, plain launches");
+        // Registers: the asm holds v0 .. v(2 SEG + 25); everything else live across the turn
+        // loop must fit the rest of the 80-VGPR budget (6 waves per SIMD): the three addresses,
+        // a scalar turn count (the turn the wave leaves the trapezoid at, computed once), and
+        // the store stage's lane values recomputed after the loop rather than kept.
+        // (k_step_tile has no static LDS: the dynamic slots start at LDS address 0, so the
+        // parity toggle is an XOR of each address with ps)
+        constexpr int TV = (GOL_TURN_VAR & 6) | (ORD == 9 ? 1 : 0);
+        const uint32_t base = (uint32_t)(uintptr_t)(lds_void *)xsh;
+        uint32_t ad[4];
+        uint32_t ps;
+        if constexpr ((TV & 4) != 0) {
+            // [parity][top, bottom][slot], 16 B per slot (nslot a power of two: host-checked)
+            const uint32_t ns = (uint32_t)nslot;
+            ad[0] = base + 16u * (uint32_t)myslot;
+            ad[1] = base + 16u * (ns + (uint32_t)myslot);
+            ad[2] = base + 16u * (ns + (uint32_t)s_up);     // the segment above's last-row sums
+            ad[3] = base + 16u * (uint32_t)s_dn;            // the segment below's first-row sums
+            ps = 32u * ns;
+        } else {
+            // [slot][top, bottom][parity], 64 B per slot
+            ad[0] = base + 64u * (uint32_t)myslot;
+            ad[1] = 0u;
+            ad[2] = base + 64u * (uint32_t)s_up + 32u;
+            ad[3] = base + 64u * (uint32_t)s_dn;
+            ps = 16u;
+        }
+        // the wave leaves at the first turn t with wrow1 <= t or wrow0 > lastrow - t
+        const int tend = __builtin_amdgcn_readfirstlane(
+            max(0, min(K, min(wrow1, lastrow - wrow0 + 1))));
+        const uint32_t ba = ORD == 9 ? (uint32_t)((lane + 63) & 63) * 4u : 0u;
+        ps = __builtin_amdgcn_readfirstlane(ps);
+        for (int t = 0; t < tend; ++t) tile_turn_asm<SEG, TV>(v, ad, ps, ba);
+        if (tend < K) return;
+        // interior rows [K, K + TH) of the tile, below row_hi; interior columns inside the row
+        // (the lane's values from the lane count of an opaque all-ones mask, formed after the
+        // loop: neither the thread index nor anything derived from it stays live across it)
+        uint32_t all = ~0u;
+        asm volatile("" : "+v"(all));
+        const int ln = (int)__builtin_amdgcn_mbcnt_hi(all, __builtin_amdgcn_mbcnt_lo(all, 0u));
+        const int gr = ln / C, cl = ln - gr * C;
+        if (gr >= G || cl < 1 || cl > TW || x0 + cl - 1 >= nl) return;
+        const int t0 = (wave * G + gr) * SEG;
+        uint32_t so = (uint32_t)(y0 - K + t0) * pitch_b + (uint32_t)(x0 + cl - 1) * 8u;
+#pragma unroll
+        for (int i = 0; i < SEG; ++i) {
+            const int tr = t0 + i;
+            if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) buf_store(v[i], rout, so, 0);
+            so += pitch_b;
+        }
+        return;
+    } else if constexpr (kHalo) {
         static_assert(!kPairs, "ORD 7: long segments");
         for (int t = 0; t < K; ++t) {
             // (wave 0 spans the whole tile and never leaves: wrow1 is out of reach)

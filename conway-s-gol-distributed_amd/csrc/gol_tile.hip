@@ -118,6 +118,20 @@ void *tile_kernel(int code)
     // ORD 7 (wave 0 holds the halo segments and skips the rows the trapezoid has left): the
     // 65536^2 segment only; tools build (it measured 0.5 % slower than ORD 5)
 #if GOL_TOOLS
+    // ORD 8 (ORD 5's turn in inline asm with a hand-made VGPR assignment): SEG 6, 12, 24
+    if (ord == 8 && w == 1) {
+        if (seg == 24) return reinterpret_cast<void *>(&k_step_tile<24, 8, 1>);
+        if (seg == 12) return reinterpret_cast<void *>(&k_step_tile<12, 8, 1>);
+        if (seg == 6) return reinterpret_cast<void *>(&k_step_tile<6, 8, 1>);
+        return nullptr;
+    }
+    // ORD 9 (ORD 8 with the lane shifts' neighbour words by ds_bpermute instead of DPP)
+    if (ord == 9 && w == 1) {
+        if (seg == 24) return reinterpret_cast<void *>(&k_step_tile<24, 9, 1>);
+        if (seg == 12) return reinterpret_cast<void *>(&k_step_tile<12, 9, 1>);
+        if (seg == 6) return reinterpret_cast<void *>(&k_step_tile<6, 9, 1>);
+        return nullptr;
+    }
     if (ord == 7) return w == 1 && seg == 24 ? reinterpret_cast<void *>(&k_step_tile<24, 7, 1>) : nullptr;
 #endif
     if (ord > 2) return nullptr;
@@ -137,7 +151,11 @@ bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
     const int nseg = (tile_h + 2 * turns + seg - 1) / seg;
     // ORD 7: two lane groups per wave (wave 0 = the top and the bottom segment), >= 3 segments
     if (ord == 7 && (G != 2 || nseg < 3)) return false;
-    return (nseg + G - 1) / G <= kTileMaxWaves;
+    const int waves = (nseg + G - 1) / G;
+    // ORD 8 / 9 with the 16-B slot layout toggle the turn parity by an XOR: a power-of-two
+    // number of slots
+    if ((ord == 8 || ord == 9) && (GOL_TURN_VAR & 4) && (waves & (waves - 1))) return false;
+    return waves <= kTileMaxWaves;
 }
 
 int tile_waves(int turns, int tile_h, int tile_w, int seg)

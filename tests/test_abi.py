@@ -166,3 +166,24 @@ def test_pinned_shapes_match_the_tests():
     want.update({(65536, 65536 // n + 256): v for n, v in T.PINNED_STRIP_SHAPES.items()})
     assert got == want
     assert all(v[3] in TILE_CODES for v in got.values())
+
+
+def test_tile_turn_header_is_generated():
+    """gol_tile_turn.h (K1t ORD 8 / 9: the turn as inline asm with a hand-made VGPR assignment)
+    is exactly what gen_tile_turn.py writes, and every v_bitop3 in it reads registers of both
+    parities (a v_bitop3 whose three sources share one register-number parity issues at half
+    rate on gfx950: profiles/r05_vgpr_bank_probe.log)."""
+    import re
+    import subprocess
+    import sys
+    csrc = os.path.join(os.path.dirname(__file__), "..", "conway-s-gol-distributed_amd", "csrc")
+    gen = subprocess.run([sys.executable, os.path.join(csrc, "gen_tile_turn.py")],
+                         capture_output=True, text=True, check=True).stdout
+    with open(os.path.join(csrc, "gol_tile_turn.h")) as f:
+        assert f.read() == gen
+    n = 0
+    for m in re.finditer(r'"v_bitop3_b32 v(\d+), v(\d+), v(\d+), v(\d+)', gen):
+        srcs = [int(m.group(i)) for i in (2, 3, 4)]
+        assert len({r % 2 for r in srcs}) == 2, m.group(0)
+        n += 1
+    assert n > 1000

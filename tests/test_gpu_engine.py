@@ -548,14 +548,16 @@ def test_driver_command_digest(gol, monkeypatch, pin):
 
 
 @tools_only
+@pytest.mark.parametrize("code", [724, 824])
 @pytest.mark.parametrize("K,key", [(20, "65536x65536_seed3_t25"), (24, "65536x65536_seed3_t1000")])
-def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key):
+def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key, code):
     """ORD 7 (code 724: wave 0 holds the tile's top segment and its bottom segment in reverse
-    row order, and skips the rows the shrinking trapezoid has left) on 30 x 336 tiles at full
-    size against the oracle digests: K = 20 (the bottom segment reaches 8 rows past the
-    loaded halo) and K = 24 (both segments are exactly the 24 halo rows)."""
+    row order, and skips the rows the shrinking trapezoid has left) and ORD 8 (code 824: the
+    turn in inline asm with a hand-made VGPR assignment) on 30 x 336 tiles at full size
+    against the oracle digests: K = 20 (ORD 7's bottom segment reaches 8 rows past the loaded
+    halo) and K = 24 (both segments are exactly the 24 halo rows)."""
     monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
-    monkeypatch.setenv("GOL_TILE", "30,724")
+    monkeypatch.setenv("GOL_TILE", f"30,{code}")
     d = _digests()[key]
     with _engine(gol, d["width"], d["height"], band_rows=336, turns_per_launch=K) as e:
         e.fill_random(d["seed"])
@@ -564,7 +566,7 @@ def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key):
             e.step(20)
         else:
             e.step(d["turns"])
-        assert {(t[0], t[1]) for t in e.last_launch_tiles()} == {(30, 724)}
+        assert {(t[0], t[1]) for t in e.last_launch_tiles()} == {(30, code)}
         assert e.snapshot() == (d["turns"], d["alive"])
         assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
 
@@ -771,7 +773,7 @@ def _pinned_shape(code):
     return (14, 100) if seg <= 8 else (30, 100)   # 66 words = 4 x 14 + 10 = 2 x 30 + 6
 
 
-@pytest.mark.parametrize("code", list(TILE_CODES) + _tools(724))
+@pytest.mark.parametrize("code", list(TILE_CODES) + _tools(724, 824, 812, 806, 924, 912, 906))
 def test_tile_code_pinned(gol, oracle, monkeypatch, code):
     """Every k_step_tile instantiation the product library can run (gol_tile_codes; the shape
     searches pick only these) against the oracle: ragged tiles in both directions, one launch

@@ -55,6 +55,12 @@ for step in "$@"; do
     ord7)   run ord7t 300 python -u -m pytest tests/test_gpu_engine.py -v --timeout 200 --timeout-method thread -k "halo_wave or test_tile_code_pinned" && run ord7ab 400 python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:20,30:336:724:20,30:336:724:24,30:344:724:20,30:336:524:24,14:720:524:24 && run ord7ab2 400 python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:724:20,30:336:524:20,30:336:724:24,30:336:524:24 ;;
     retune16) run retune16 400 env GOL_AUTOTUNE=2 GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 16384 --auto --turns 640 --rounds 3 --shapes 14:316:106:32,14:320:108:32,14:316:206:32,14:320:112:32,14:352:512:16,14:316:506:32,30:320:512:32,30:320:112:32,30:320:516:32,30:352:516:16,14:448:108:32,14:456:112:24 ;;
     retune5) run retune5 300 env GOL_AUTOTUNE=2 GOL_AUTOTUNE_LOG=1 python -u tools/tile_sweep.py --size 5120 --auto --turns 960 --rounds 3 --shapes 14:128:203:32,14:128:104:32,14:128:204:32,14:128:106:32,10:160:104:32,14:128:504:32,14:160:104:32 ;;
+    bank)   run bank 200 tools/calib/vgpr_bank_probe 2000 ;;
+    deep65) run deep65 500 python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:592:540:24,30:600:540:20,30:561:540:24,30:616:540:12,30:608:540:16,30:464:532:24,30:472:532:20,30:552:524:12,30:528:524:24,30:336:524:24 ;;
+    ord8)   run ord8t 400 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u -m pytest tests/test_gpu_engine.py -v --timeout 200 --timeout-method thread -k "halo_wave or (test_tile_code_pinned and (824 or 812 or 806 or 524))" && run ord8ab 500 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:336:824:24,30:336:824:20,30:336:524:20,30:336:824:24 && run ord8s 500 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 65536 --height 8448 --turns 128 --rounds 3 --shapes 14:352:512:16,14:352:812:16,14:352:512:16,14:352:812:16 && run ord8s4 500 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 65536 --height 16640 --turns 128 --rounds 3 --shapes 14:704:524:32,14:704:824:32,14:704:524:32,14:704:824:32 && run ord8c3 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 16384 --turns 640 --rounds 3 --shapes 14:316:106:32,14:316:806:32,14:316:106:32,14:316:806:32 ;;
+    iso)    run iso 300 tools/calib/turn_issue 3000 3 ;;
+    ord9)   run ord9t 400 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u -m pytest tests/test_gpu_engine.py -v --timeout 200 --timeout-method thread -k "test_tile_code_pinned and (924 or 912 or 906)" && run ord9ab 500 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:336:924:24,30:336:824:24,30:336:524:24 ;;
+    tvab)   for r in 1 2; do for V in 0 2 4 6; do run tvab_${V}_$r 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tv$V.so python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:336:824:24,30:336:924:24; done; done ;;
     fullnx) run fullnx 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
