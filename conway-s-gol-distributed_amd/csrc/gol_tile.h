@@ -52,7 +52,7 @@
 // rows 1 and 2 instead of right after the edge sums' stores, bit 2 = LDS slots 16 B apart
 // instead of 64 (A/B builds: make variant VDEFS=-DGOL_TURN_VAR=n)
 #ifndef GOL_TURN_VAR
-#define GOL_TURN_VAR 0
+#define GOL_TURN_VAR 4
 #endif
 #ifndef GOL_TILE_WEST_CARRY
 #define GOL_TILE_WEST_CARRY 1
@@ -76,9 +76,26 @@ constexpr size_t tile_lds_bytes(int threads, int words)
 // published edge sums, through per-wave progress flags in LDS; 5: ORD 1 with the edge sums
 // read back from LDS instead of kept in registers; 6: ORD 5 with the barrier after the
 // interior rows; 7: ORD 5 with the tile's two halo segments in wave 0, which skips the rows
-// the shrinking trapezoid no longer needs -- see tile_pass), words per lane
+// the shrinking trapezoid no longer needs -- see tile_pass; 8: ORD 5's turn as generated
+// inline asm with a hand-made, parity-aware VGPR assignment; 9: ORD 8 with ds_bpermute lane
+// shifts -- 7, 8 and 9 in the tools build only), words per lane
 constexpr int tile_seg_rows(int code) { return code % 100; }
 constexpr int tile_seg_words(int code) { return code / 1000 + 1; }
+// ORD 8 / 9 with the 16-B slot layout: the slot count rounded up to a power of two (the turn
+// parity is an XOR of the addresses)
+constexpr int tile_slots_pow2(int threads)
+{
+    int n = 64;
+    while (n < threads) n *= 2;
+    return n;
+}
+constexpr size_t tile_lds_bytes_code(int threads, int code)
+{
+    const int ord = code / 100 % 10;
+    return (ord == 8 || ord == 9) && (GOL_TURN_VAR & 4)
+               ? tile_lds_bytes(tile_slots_pow2(threads), 1)
+               : tile_lds_bytes(threads, tile_seg_words(code));
+}
 
 // W words per lane (2W dwords, interleaved layout word by word).  With W = 2 the lane's two
 // words are neighbours, so only the outer edges need a lane shift: per row 2 DPP + 2W funnel
@@ -478,8 +495,9 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         uint32_t ad[4];
         uint32_t ps;
         if constexpr ((TV & 4) != 0) {
-            // [parity][top, bottom][slot], 16 B per slot (nslot a power of two: host-checked)
-            const uint32_t ns = (uint32_t)nslot;
+            // [parity][top, bottom][slot], 16 B per slot, the slot count a power of two
+            // (tile_lds_bytes_code)
+            const uint32_t ns = (uint32_t)tile_slots_pow2(nslot);
             ad[0] = base + 16u * (uint32_t)myslot;
             ad[1] = base + 16u * (ns + (uint32_t)myslot);
             ad[2] = base + 16u * (ns + (uint32_t)s_up);     // the segment above's last-row sums

@@ -152,9 +152,6 @@ bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
     // ORD 7: two lane groups per wave (wave 0 = the top and the bottom segment), >= 3 segments
     if (ord == 7 && (G != 2 || nseg < 3)) return false;
     const int waves = (nseg + G - 1) / G;
-    // ORD 8 / 9 with the 16-B slot layout toggle the turn parity by an XOR: a power-of-two
-    // number of slots
-    if ((ord == 8 || ord == 9) && (GOL_TURN_VAR & 4) && (waves & (waves - 1))) return false;
     return waves <= kTileMaxWaves;
 }
 
@@ -180,7 +177,7 @@ int tile_blocks_per_cu(int turns, int tile_h, int tile_w, int seg)
     if (it != cache.end()) return it->second;
     int blocks = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks, fn, 64 * waves, tile_lds_bytes(64 * waves, tile_seg_words(seg))) != hipSuccess)
+            &blocks, fn, 64 * waves, tile_lds_bytes_code(64 * waves, seg)) != hipSuccess)
         blocks = 0;
     cache[{seg, waves}] = blocks;
     return blocks;
@@ -209,7 +206,7 @@ hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s)
     int k = turns, ntx_arg = ntx, nt = (int)ntiles;
     void *params[] = {&in, &out, &args, &k, &ntx_arg, &nt};
     return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params,
-                           tile_lds_bytes(threads, tile_seg_words(a.tile_seg)), s);
+                           tile_lds_bytes_code(threads, a.tile_seg), s);
 }
 
 }  // namespace golk
