@@ -36,19 +36,20 @@ Usage: python3 gen_tile_turn.py > gol_tile_turn.h  (the Makefile does this)
 import sys
 
 SEGS = (24, 12, 6)
-VARIANTS = range(8)
+VARIANTS = (4, 5)        # the tools build's ORD 8 / 9 (GOL_TURN_VAR = 4); add others for A/B builds
 
 
 class Gen:
     def __init__(self, seg, var=0, iso=False):
-        assert seg % 3 == 0 and seg >= 6 and 0 <= var < 8
+        assert seg % 3 == 0 and seg >= 6 and 0 <= var < 16
         mode = "bperm" if var & 1 else "dpp"
-        assert not (iso and var)
+        assert not (iso and var & 7)
         self.seg = seg
         self.var = var
         self.mode = mode
         self.late = bool(var & 2)    # barrier after rows 1 and 2 (ORD 5's compiled placement)
         self.dense = bool(var & 4)   # LDS slots 16 B apart (ORD 5's layout) instead of 64
+        self.ahead = bool(var & 8)   # DPP moves issued two rows ahead (double-buffered)
         self.iso = iso          # timing harness: the turn without LDS and barrier (wrong board)
         self.lq = []            # outstanding LDS operations, in issue order (tags)
         self.out = []
@@ -66,7 +67,7 @@ class Gen:
         self.nregs = b + 26
         # bperm: the lane-shifted words arrive by ds_bpermute_b32 one row ahead, double-buffered
         self.bufs = [(self.TA, self.TB), (b + 26, b + 27)]
-        if mode == "bperm":
+        if mode == "bperm" or self.ahead:
             self.nregs = b + 28
         self.free = list(self.bufs)
         self.pending = {}       # row -> buffer its shifted words are (or will be) in
@@ -112,11 +113,19 @@ class Gen:
         self.lq = []
 
     def issue_shift(self, row):
-        """bperm: the west lane's odd dword and the east lane's even dword of `row`."""
-        if self.mode != "bperm":
+        """bperm: the west lane's odd dword and the east lane's even dword of `row`; dpp with
+        `ahead`: the same by DPP moves, issued early."""
+        if self.mode != "bperm" and not self.ahead:
             return
         A, B = self.free.pop(0)
         e, o = 2 * row, 2 * row + 1
+        if self.mode == "dpp":
+            self.emit("v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, o),
+                      (o,), (A,), dpp_src=o)
+            self.emit("v_mov_b32_dpp v%d, v%d wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (B, e),
+                      (e,), (B,), dpp_src=e)
+            self.pending[row] = (A, B)
+            return
         self.lds("ds_bpermute_b32 v%d, %%[ba], v%d" % (A, o), ("w", row), (o,), (A,))
         self.lds("ds_bpermute_b32 v%d, %%[ba], v%d offset:8" % (B, e), ("e", row), (e,), (B,))
         self.pending[row] = (A, B)
@@ -133,6 +142,8 @@ class Gen:
         if self.mode == "bperm":
             A, B = self.pending.pop(row)
             self.wait_for(("e", row))
+        elif self.ahead:
+            A, B = self.pending.pop(row)
         else:
             A, B = self.TA, self.TB
             self.emit("v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, o),
@@ -145,7 +156,7 @@ class Gen:
         self.bitop3(S[1], A, e, o, 0xE8)
         self.bitop3(S[2], e, o, B, 0x96)
         self.bitop3(S[3], e, o, B, 0xE8)
-        if self.mode == "bperm":
+        if self.mode == "bperm" or self.ahead:
             self.free.append((A, B))
 
     def rule(self, row, P, Q, R):
@@ -232,16 +243,16 @@ class Gen:
         if self.iso:
             return """
 // SEG %d, timing harness only (tools/calib/turn_issue.hip): the dpp turn without its LDS
-// exchange and barrier
+// exchange and barrier (variant %d: 8 = DPP moves two rows ahead)
 template <>
-__device__ __forceinline__ void tile_turn_iso<%d>(uint32_t (&v)[%d][2])
+__device__ __forceinline__ void tile_turn_iso<%d, %d>(uint32_t (&v)[%d][2])
 {
     asm volatile(
 %s        : %s
         :
         : %s);
 }
-""" % (s, s, s, body, ops, clob)
+""" % (s, self.var, s, self.var, s, body, ops, clob)
         nbp = sum(1 for l in self.out if l.startswith("ds_bpermute"))
         outs = ['[me] "+v"(ad[0])'] + (['[mb] "+v"(ad[1])'] if self.dense else []) + \
                ['[up] "+v"(ad[2])', '[dn] "+v"(ad[3])']
@@ -286,10 +297,11 @@ __device__ __forceinline__ void tile_turn_asm(uint32_t (&v)[SEG][2], uint32_t (&
             parts.append(Gen(s, var).header())
     parts.append("""
 #ifdef GOL_TURN_ISO
-template <int SEG> __device__ __forceinline__ void tile_turn_iso(uint32_t (&v)[SEG][2]);
+template <int SEG, int V> __device__ __forceinline__ void tile_turn_iso(uint32_t (&v)[SEG][2]);
 """)
     for s in SEGS:
-        parts.append(Gen(s, iso=True).header())
+        for var in (0, 8):
+            parts.append(Gen(s, var, iso=True).header())
     parts.append("#endif\n")
     parts.append("\n}  // namespace golk\n")
     sys.stdout.write("".join(parts))

@@ -38,7 +38,7 @@ __device__ __forceinline__ void rule(const uint32_t (&A)[4], const uint32_t (&B)
     x[1] = n1;
 }
 
-template <int SEG, bool HAND>
+template <int SEG, int HAND>
 __global__ __launch_bounds__(256, 6) void k_turn(uint32_t *out, unsigned long long *clk, int turns)
 {
     extern __shared__ uint32_t pad[];
@@ -53,8 +53,8 @@ __global__ __launch_bounds__(256, 6) void k_turn(uint32_t *out, unsigned long lo
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     for (int t = 0; t < turns; ++t) {
-        if constexpr (HAND) {
-            tile_turn_iso<SEG>(v);
+        if constexpr (HAND >= 0) {
+            tile_turn_iso<SEG, HAND>(v);
         } else {
             uint32_t first[4], last[4], P[4], Q[4];
             rsum(v[SEG - 1], last);
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256, 6) void k_turn(uint32_t *out, unsigned long lo
     }
 }
 
-template <int SEG, bool HAND>
+template <int SEG, int HAND>
 static void run(int W, int turns, int ncu, int reps)
 {
     auto fn = k_turn<SEG, HAND>;
@@ -132,7 +132,7 @@ static void run(int W, int turns, int ncu, int reps)
     const double cyc = best * 1e-3 * clock * 1e9 / ((double)W * valu_per_wave);
     std::printf("{\"body\": \"%s\", \"seg\": %d, \"waves_per_simd\": %d, \"vgprs\": %d, \"kernel_ms\": %.4f, "
                 "\"clock_ghz\": %.3f, \"simd_cycles_per_valu\": %.4f, \"cycles_per_row\": %.2f}\n",
-                HAND ? "hand-assigned asm (ORD 8)" : "compiler (ORD 5 stream)", SEG, W, attr.numRegs,
+                HAND < 0 ? "compiler (ORD 5 stream)" : HAND ? "hand-assigned asm, DPP two rows ahead" : "hand-assigned asm (ORD 8)", SEG, W, attr.numRegs,
                 best, clock, cyc, cyc * 22.0);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
@@ -147,14 +147,17 @@ int main(int argc, char **argv)
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
     for (int W : {4, 6}) {
-        run<24, false>(W, turns, ncu, reps);
-        run<24, true>(W, turns, ncu, reps);
+        run<24, -1>(W, turns, ncu, reps);
+        run<24, 0>(W, turns, ncu, reps);
+        run<24, 8>(W, turns, ncu, reps);
     }
     for (int W : {4, 8}) {
-        run<12, false>(W, turns, ncu, reps);
-        run<12, true>(W, turns, ncu, reps);
-        run<6, false>(W, turns, ncu, reps);
-        run<6, true>(W, turns, ncu, reps);
+        run<12, -1>(W, turns, ncu, reps);
+        run<12, 0>(W, turns, ncu, reps);
+        run<12, 8>(W, turns, ncu, reps);
+        run<6, -1>(W, turns, ncu, reps);
+        run<6, 0>(W, turns, ncu, reps);
+        run<6, 8>(W, turns, ncu, reps);
     }
     return 0;
 }

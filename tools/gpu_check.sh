@@ -64,6 +64,7 @@ for step in "$@"; do
     pmc8)   for c in 524 824 924; do lib=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tv4.so; run pmc8_$c 400 env TAG=_$c GOL_AMD_LIB=$lib bash tools/pmc_sq.sh tools/kernel_run.py --size 65536 --mv 15 --tpl 24 --band 336 --tile 30,$c --turns 48; done ;;
     ord89)  run ord89t 500 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u -m pytest tests/test_gpu_engine.py -v --timeout 200 --timeout-method thread -k "halo_wave or (test_tile_code_pinned and (824 or 812 or 806 or 924 or 912 or 906))" ;;
     strip4c) run strip4c 500 python -u tools/tile_sweep.py --size 65536 --height 16640 --turns 144 --rounds 3 --shapes 14:704:524:32,30:336:524:24,30:320:524:24,30:330:524:24,30:347:524:24,14:720:524:24,14:694:524:32,30:336:524:20,14:704:524:32 && run strip2c 500 python -u tools/tile_sweep.py --size 65536 --height 33024 --turns 96 --rounds 3 --shapes 14:704:524:32,30:336:524:24,30:344:524:24,30:333:524:24,14:720:524:24,30:336:524:20,14:704:524:32 ;;
+    ahead)  run iso2 300 tools/calib/turn_issue 3000 3 && for r in 1 2; do run ahead_t_$r 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:336:824:24 && run ahead_v_$r 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tv12.so python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:336:824:24; done ;;
     fullnx) run fullnx 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
