@@ -219,17 +219,19 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier(device_ids=dev_ids)
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
 
-    t0 = time.perf_counter()
+    # (ev0 is recorded on the idle stream just before the clock starts: its host call is
+    # instrumentation, not part of the timed steps; ev1's overlaps the running kernels)
     ev0.record(stream)
+    t0 = time.perf_counter()
     runner.step(steps)
     ev1.record(stream)
     alive = eng.snapshot() if snapshot else None
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier(device_ids=dev_ids)
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
     plan = eng.last_launches()          # the last gol_step call's launches (N > 1: one window)

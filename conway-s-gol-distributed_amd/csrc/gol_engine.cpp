@@ -1034,11 +1034,42 @@ bool verify_pinned(gol_ctx *c, const KnownShape &ks)
                                  c->buf_rows, 12345, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return false;
-    // bursts of ~1 ms of launches, each ended by a sync (host wall time, as gol_step runs)
+    // groups of ~1 ms of launches
     const int n = std::max(1, (int)std::ceil(1000.0 / (ks.t.K * ks.us_per_turn)));
     std::vector<float> us;
+    // (default) one queue of back-to-back launches, an event pair per group, one sync at the
+    // end: the GPU stays busy for the whole check (bench20 116.5-118.0k against 116.1-117.2k
+    // with a sync after every burst, profiles/r05_verify_mode_ab.log); GOL_PIN_VERIFY_MODE=0:
+    // bursts of ~1 ms, each ended by a sync
+    const char *vm = getenv("GOL_PIN_VERIFY_MODE");
+    const bool queued = !(vm && atoi(vm) == 0);
+    if (queued) {
+        const int groups = std::max(8, (int)std::ceil(budget_ms * 1000.0 / (n * ks.t.K * ks.us_per_turn)));
+        std::vector<hipEvent_t> ev(groups + 1);
+        for (auto &e : ev)
+            if (hipEventCreate(&e) != hipSuccess) return false;
+        bool ok = hipEventRecord(ev[0], c->stream) == hipSuccess;
+        for (int i = 0; ok && i < groups; ++i) {
+            for (int j = 0; ok && j < n; ++j) {
+                a.in = c->board[j & 1];
+                a.out = c->board[(j + 1) & 1];
+                ok = golk::launch_step_multi(a, ks.t.K, c->stream) == hipSuccess;
+            }
+            ok = ok && hipEventRecord(ev[i + 1], c->stream) == hipSuccess;
+        }
+        ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
+        for (int i = 0; ok && i < groups; ++i) {
+            float ms = 0.f;
+            ok = hipEventElapsedTime(&ms, ev[i], ev[i + 1]) == hipSuccess;
+            us.push_back(ms * 1e3f / (n * ks.t.K));
+        }
+        for (auto &e : ev) (void)hipEventDestroy(e);
+        if (!ok) return false;
+    }
+    // GOL_PIN_VERIFY_MODE=0: bursts of ~1 ms of launches, each ended by a sync (host wall time,
+    // as gol_step runs)
     const auto t0 = std::chrono::steady_clock::now();
-    for (int i = 0; i < 2000; ++i) {
+    for (int i = 0; !queued && i < 2000; ++i) {
         const auto s0 = std::chrono::steady_clock::now();
         for (int j = 0; j < n; ++j) {
             a.in = c->board[j & 1];

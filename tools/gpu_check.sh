@@ -65,6 +65,9 @@ for step in "$@"; do
     ord89)  run ord89t 500 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u -m pytest tests/test_gpu_engine.py -v --timeout 200 --timeout-method thread -k "halo_wave or (test_tile_code_pinned and (824 or 812 or 806 or 924 or 912 or 906))" ;;
     strip4c) run strip4c 500 python -u tools/tile_sweep.py --size 65536 --height 16640 --turns 144 --rounds 3 --shapes 14:704:524:32,30:336:524:24,30:320:524:24,30:330:524:24,30:347:524:24,14:720:524:24,14:694:524:32,30:336:524:20,14:704:524:32 && run strip2c 500 python -u tools/tile_sweep.py --size 65536 --height 33024 --turns 96 --rounds 3 --shapes 14:704:524:32,30:336:524:24,30:344:524:24,30:333:524:24,14:720:524:24,30:336:524:20,14:704:524:32 ;;
     ahead)  run iso2 300 tools/calib/turn_issue 3000 3 && for r in 1 2; do run ahead_t_$r 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tools.so python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:336:824:24 && run ahead_v_$r 300 env GOL_AMD_LIB=$PWD/conway-s-gol-distributed_amd/build/libgolamd_tv12.so python -u tools/tile_sweep.py --size 65536 --turns 120 --rounds 3 --shapes 30:336:524:24,30:336:824:24; done ;;
+    th344)  for r in 1 2; do run th344_$r 400 python -u tools/tile_sweep.py --size 65536 --turns 240 --rounds 3 --shapes 30:336:524:24,30:344:524:20,30:336:524:20,30:340:524:20,30:344:524:20,30:336:524:24; done ;;
+    svs)    run svs 300 python -u tools/single_vs_seq.py && (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/svs_kt" -o run --output-format csv -- python3 "$OLDPWD/tools/single_vs_seq.py" > "$OLDPWD/gpurun_out/svs_kt.log" 2>&1); echo "svs kt rc=$?" ;;
+    vmode)  for i in 1 2 3; do run b20m0_$i 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1 && run b20m1_$i 200 env GOL_PIN_VERIFY_MODE=1 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --c3-size 0 --c2-size 0 --no-c1; done ;;
     fullnx) run fullnx 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ;;
     full)   run full 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread ;;
     stripx) run stripx 500 env GOL_AUTOTUNE_LOG=1 python -u tools/strip_emulate.py --n 2,4,8 --halo 128 --rccl direct --full --turns 768 ;;
