@@ -350,7 +350,7 @@ def measure_c1(gpu, stream):
         exact = exact and bool(np.array_equal(got, want))
         best = dt if best is None else min(best, dt)
     plan = eng.last_launches()
-    tiles = eng.last_launch_tiles()
+    tiles = eng.last_launch_tiles(blocks=True)
     eng.close()
     _, kvar, kd = kernel_depth(plan, 0)
     return {"workload": "512x512 Local/images/512x512.pgm, 100 turns (BASELINE configs[0]) "

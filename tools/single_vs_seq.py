@@ -60,3 +60,26 @@ per = [x.elapsed_time(y) * 1e3 for x, y in pairs]
 print("back to back, each evented:", [round(p) for p in per], "median %.1f" % statistics.median(per),
       flush=True)
 e.close()
+
+# (d) fresh random board against an evolved one, alternating, after the same GPU load: both
+# run 1200 turns first; "fresh" then refills the board (one fast kernel) -- is the single
+# call's cost data-dependent (its instruction stream is not)?
+e = gol.Engine(65536, 65536, device=0)
+e.set_stream(s.cuda_stream)
+res = {"fresh": [], "evolved": []}
+for rep in range(4):
+    for kind in ("fresh", "evolved"):
+        e.fill_random(3 + rep)
+        for _ in range(60):
+            e.step(20)
+        if kind == "fresh":
+            e.fill_random(3 + rep)
+        e.step(5)
+        torch.cuda.synchronize()
+        a = ev()
+        e.step(20)
+        b = ev()
+        torch.cuda.synchronize()
+        res[kind].append(round(a.elapsed_time(b) * 1e3))
+print("fresh vs evolved board, single 20-turn calls (us):", res, flush=True)
+e.close()
