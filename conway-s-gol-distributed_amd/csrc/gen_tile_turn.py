@@ -33,9 +33,11 @@ below, s_nop inserted if a schedule ever needs one.
 
 Usage: python3 gen_tile_turn.py > gol_tile_turn.h  (the Makefile does this)
 """
+import os
 import sys
 
 SEGS = (24, 12, 6)
+ALIGN = int(os.environ.get("GOL_TURN_ALIGN", "0"))   # log2 bytes, 0: none (A/B builds only)
 VARIANTS = (4, 5)        # the tools build's ORD 8 / 9 (GOL_TURN_VAR = 4); add others for A/B builds
 
 
@@ -185,6 +187,9 @@ class Gen:
         # just before the block: 2 wait states before a DPP reads one)
         if not self.iso:
             self.out.append("s_waitcnt lgkmcnt(0)")
+        if ALIGN:
+            # (A/B: the block's code alignment -- ORD 8's speed changed from build to build)
+            self.out.append(".p2align %d" % ALIGN)
         self.out.append("s_nop 1")
         # own edge rows' sums to LDS, one barrier
         self.issue_shift(0)
