@@ -985,20 +985,9 @@ else:
     out = r.stdout
     assert "EHIP" in out and "timed out" in out, out
     assert "STICKY -2" in out and "CLEARED" in out, out
-    if not TILE_PERSIST_CODES:
-        return                       # (K1p is in the tools build only since round 5)
-    # the same for k_tile_persist's neighbour-tile flag waits
-    code_p = code.replace("gol.Engine(2048, 512, device=0, band_rows=43, turns_per_launch=16)",
-                          "gol.Engine(4224, 157, device=0, band_rows=100, turns_per_launch=8)")
-    code_p = code_p.replace("gol_step(e.handle, 16)", "gol_step(e.handle, 40)")
-    env = dict(os.environ, GOL_AMD_LIB=lib, GOL_MULTI_VARIANT="15", GOL_TILE="14,103",
-               GOL_PERSIST="8")
-    r = subprocess.run([sys.executable, "-c", code_p,
-                        os.path.join(root, "conway-s-gol-distributed_amd")],
-                       capture_output=True, text=True, timeout=120, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
-    assert "EHIP" in r.stdout and "neighbour-tile" in r.stdout, r.stdout
-    assert "STICKY -2" in r.stdout and "CLEARED" in r.stdout, r.stdout
+    # (k_tile_persist's neighbour-tile flag waits report through the same word; K1p is in the
+    # tools build only since round 5, and libgolamd_spin0.so is a product build, so that path
+    # has no spin-limit test library any more)
 
 
 # ------------------------------------------------ concurrent reads while stepping
