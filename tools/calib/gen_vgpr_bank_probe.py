@@ -13,11 +13,13 @@ s_memtime span over its loop gives
 Usage: python3 gen_vgpr_bank_probe.py > vgpr_bank_probe.hip
        hipcc --offload-arch=gfx950 -O3 -o vgpr_bank_probe vgpr_bank_probe.hip
 """
+import os
 
 
 def pattern(v, i):
     d = 48 + i % 16
     k = (i % 10) * 4                     # base register: bank 0 if banks are (index mod 4)
+    A, B = 48 + (2 * i) % 16, 49 + (2 * i) % 16          # rotating DPP destinations
     b3 = "v_bitop3_b32 v%d, v%d, v%d, v%d bitop3:0x96"
     return {
         0: b3 % (d, k, k + 1, k + 2),
@@ -54,6 +56,42 @@ def pattern(v, i):
         31: ("v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (d, k)) if i % 4 == 0 else b3 % (d, k, k + 1, k + 2),
         32: "v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (d, k),
         33: "v_xor_b32_sdwa v%d, v%d, v%d dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD" % (d, k, k + 1),
+        # the stencil's lane-shift pairs (4 instructions per slot): DPP A, DPP B, then each
+        # v_alignbit reading its DPP result -- 2 instructions later (the generated ORD 8 turn),
+        # right after (the compiler's ORD 5), or 4 later with two bitop3 between
+        34: "|".join(["v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, k + 1),
+                      "v_mov_b32_dpp v%d, v%d wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (B, k),
+                      "v_alignbit_b32 v%d, v%d, v%d, 31" % (A, k + 1, A),
+                      "v_alignbit_b32 v%d, v%d, v%d, 1" % (B, B, k)]),
+        35: "|".join(["v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, k + 1),
+                      "v_alignbit_b32 v%d, v%d, v%d, 31" % (A, k + 1, A),
+                      "v_mov_b32_dpp v%d, v%d wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (B, k),
+                      "v_alignbit_b32 v%d, v%d, v%d, 1" % (B, B, k)]),
+        36: "|".join(["v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, k + 1),
+                      "v_mov_b32_dpp v%d, v%d wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (B, k),
+                      b3 % (d, k, k + 1, k + 2), b3 % (d + 1 if d < 63 else 48, k + 1, k + 2, k + 3),
+                      "v_alignbit_b32 v%d, v%d, v%d, 31" % (A, k + 1, A),
+                      "v_alignbit_b32 v%d, v%d, v%d, 1" % (B, B, k)]),
+        # the same DPP pairs with fixed destinations (ORD 8 uses one register pair for every row)
+        # 6 half-rate (3 DPP, 3 v_alignbit) and 18 full-rate v_bitop3 per 24 slots: grouped
+        # (the half-rate ones first) or spread (one every 4 slots)
+        38: (["v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, k + 1),
+              "v_alignbit_b32 v%d, v%d, v%d, 31" % (B, k + 1, k)][i % 2] if i % 24 < 6
+             else b3 % (d, k, k + 1, k + 2)),
+        39: (["v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, k + 1),
+              "v_alignbit_b32 v%d, v%d, v%d, 31" % (B, k + 1, k)][(i // 4) % 2] if i % 4 == 0
+             else b3 % (d, k, k + 1, k + 2)),
+        # 2 half-rate per 24 (one DPP, one v_alignbit), grouped or spread
+        40: (["v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, k + 1),
+              "v_alignbit_b32 v%d, v%d, v%d, 31" % (B, k + 1, k)][i % 2] if i % 24 < 2
+             else b3 % (d, k, k + 1, k + 2)),
+        41: (["v_mov_b32_dpp v%d, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (A, k + 1),
+              "v_alignbit_b32 v%d, v%d, v%d, 31" % (B, k + 1, k)][(i // 12) % 2] if i % 12 == 0
+             else b3 % (d, k, k + 1, k + 2)),
+        37: "|".join(["v_mov_b32_dpp v56, v%d wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % (k + 1),
+                      "v_mov_b32_dpp v61, v%d wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" % k,
+                      "v_alignbit_b32 v56, v%d, v56, 31" % (k + 1),
+                      "v_alignbit_b32 v61, v61, v%d, 1" % k]),
     }[v]
 
 
@@ -67,7 +105,12 @@ NAMES = [
     "bitop3 2 vgpr (banks 0,1) + sgpr", "bitop3 2 vgpr (banks 0,0) + sgpr", "alignbit same reg",
     "v_alignbyte_b32", "v_cmp_ne_u32_e64 sgpr pair", "carry west shift (cmp, s_lshl, addc) / bitop3 alt",
     "1 DPP mov per 4 (3 bitop3)", "v_mov_b32_dpp wave_shr", "v_xor_b32_sdwa",
+    "DPP,DPP,align(2 later),align (ORD 8 order)", "DPP,align,DPP,align (compiler order)",
+    "DPP,DPP,2 bitop3,align,align", "DPP pairs, fixed dst v56/v61 (ORD 8 registers)",
+    "6 half-rate grouped + 18 bitop3 (per 24)", "6 half-rate spread 1-in-4 + 18 bitop3",
+    "2 half-rate grouped + 22 bitop3 (per 24)", "2 half-rate spread 1-in-12 + 22 bitop3",
 ]
+ONLY = [int(x) for x in os.environ.get("PROBE_ONLY", "").split(",") if x]
 NV = len(NAMES)
 NI = 128
 
@@ -118,13 +161,15 @@ __global__ __launch_bounds__(1024) void k_probe%d(unsigned *out, unsigned long l
 
 out.append("static void *kFn[] = {%s};\n" % ", ".join("(void *)&k_probe%d" % v for v in range(NV)))
 out.append("static const char *kName[] = {%s};\n" % ", ".join('"%s"' % n for n in NAMES))
+RUN = ONLY or list(range(NV))
+out.append("static const int kRun[] = {%s};\n" % ", ".join(str(v) for v in RUN))
 out.append("""
 int main(int argc, char **argv)
 {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     int ncu = 0;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
-    for (int v = 0; v < %d; ++v) {
+    for (int v : kRun) {
         for (int W : {1, 2, 3, 4, 6, 8}) {
             // W waves per SIMD: workgroups of 4 x min(W, 4) waves, LDS so that W / 4 of them
             // (or one) fit a CU; the per-SIMD spans below show what was co-resident
@@ -180,5 +225,5 @@ int main(int argc, char **argv)
     }
     return 0;
 }
-""" % (NV, NI, NI))
+""" % (NI, NI))
 print("".join(out))
