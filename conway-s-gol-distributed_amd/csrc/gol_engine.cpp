@@ -975,9 +975,10 @@ constexpr KnownShape kKnownShapes[] = {
     // (profiles/r04_sweep_65536_ord5.log, r04_sweep_65536_fine.log; K = 24 ~1 % ahead of K = 20,
     // profiles/r05_ord7_ab.log); the driver's 20-turn call is one 20-turn launch of this shape
     {65536, 65536, {24, 336, 30, 524, 0}, 34.0f},
-    // configs[2]: ORD 1, SEG 6, 16-wave workgroups (8 waves per SIMD), two residency rounds;
-    // 2.94-3.02 us per turn (BENCH_r04 configs_measured)
-    {16384, 16384, {32, 316, 14, 106, 0}, 2.96f},
+    // configs[2]: ORD 1, SEG 12 (west carry), 8-wave workgroups, 14 x 320 tiles; 2.84-2.92 us
+    // per turn against 3.06-3.20 for round 4's ORD 1 SEG 6 16-wave pick on the same boxes
+    // (profiles/r05_c3_codes_ab.log, two boxes; a third had them level, r05_retune_16384.log)
+    {16384, 16384, {32, 320, 14, 112, 0}, 2.88f},
     // configs[1]: ORD 2, SEG 3, 16-wave workgroups; 0.57-0.59 us per turn (BENCH_r04)
     {5120, 5120, {32, 128, 14, 203, 0}, 0.58f},
     // configs[3..4] as row strips with the bench's 128-row halos (buffer = H / N + 256 rows):
