@@ -985,7 +985,9 @@ constexpr KnownShape kKnownShapes[] = {
     // N = 8 ORD 5 SEG 12 on 352-row tiles, 8 launches of 16 turns per window (5.23-5.63 us
     // per turn against 5.61-5.71 for round 4's searched picks); N = 4 and 2 ORD 5 SEG 24 on
     // 14 x 704 tiles (tile sweeps over the strip shapes, profiles/r05_strip_sweep.log)
-    {65536, 8448, {16, 352, 14, 512, 0}, 5.3f},
+    // (N = 8: ORD 1 SEG 12 since late round 5 -- 5.44-5.46 against 5.69-5.70 us per turn for
+    // ORD 5 SEG 12 on the same tiles, profiles/r05_strip_seg12_ab.log)
+    {65536, 8448, {16, 352, 14, 112, 0}, 5.3f},
     {65536, 16640, {32, 704, 14, 524, 0}, 9.5f},
     {65536, 33024, {32, 704, 14, 524, 0}, 18.4f},
 };
