@@ -746,6 +746,10 @@ void gol_run::run()
     close();
 }
 
+// why the calling thread's last gol_run_start failed after it had validated its arguments
+// (gol_run_error(NULL)); cleared by a start that succeeds
+thread_local std::string t_start_error;
+
 extern "C" {
 
 int gol_run_start(const gol_params *p, const gol_run_options *o, gol_run **out)
@@ -777,20 +781,40 @@ int gol_run_start(const gol_params *p, const gol_run_options *o, gol_run **out)
             delete r;
             return GOL_ENODEV;
         }
-    // peer access between the strips' devices (xGMI); same-device strips need none
+    // peer access between the strips' devices (xGMI); same-device strips need none.  A device
+    // pair that reports peer access but refuses to enable it fails the start with GOL_EHIP and
+    // the reason in gol_run_error(NULL) -- the reference's dial-or-fatal for a SubServer it
+    // cannot reach (Server/gol/distributor.go:87-97) -- instead of halo copies that fail or
+    // silently stage through the host later.  A pair without peer access at all still runs:
+    // hipMemcpyPeerAsync stages its copies.
     for (size_t i = 0; i < r->devices.size(); i++)
         for (size_t j = 0; j < r->devices.size(); j++) {
             const int a = r->devices[i], b = r->devices[j];
+            if (a == b) continue;
             int can = 0;
-            if (a != b && hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can) {
+            const hipError_t qe = hipDeviceCanAccessPeer(&can, a, b);
+            int rc = GOL_OK;
+            char msg[256];
+            if (qe != hipSuccess) {
+                rc = gol_internal_peer_access_status("hipDeviceCanAccessPeer", (int)qe,
+                                                     hipGetErrorName(qe), a, b, msg, sizeof msg);
+            } else if (can) {
                 int prev = 0;
                 (void)hipGetDevice(&prev);
                 (void)hipSetDevice(a);
-                (void)hipDeviceEnablePeerAccess(b, 0);   // already-enabled is fine
+                const hipError_t pe = hipDeviceEnablePeerAccess(b, 0);
                 (void)hipGetLastError();
                 (void)hipSetDevice(prev);
+                rc = gol_internal_peer_access_status("hipDeviceEnablePeerAccess", (int)pe,
+                                                     hipGetErrorName(pe), a, b, msg, sizeof msg);
+            }
+            if (rc != GOL_OK) {
+                t_start_error = msg;
+                delete r;
+                return rc;
             }
         }
+    t_start_error.clear();
     r->th = std::thread([r] { r->run(); });
     *out = r;
     return GOL_OK;
@@ -836,9 +860,27 @@ int gol_run_key(gol_run *r, int32_t rune)
     return GOL_OK;
 }
 
+// The result of one peer-access call between two strips' devices, mapped to a return code and
+// a message: success and "already enabled" (an earlier run in the process enabled it) are
+// GOL_OK, anything else GOL_EHIP with the call, the HIP error and the device pair.  Pure (no
+// HIP call), so the CPU tests check the mapping (tests/test_abi.py).
+int gol_internal_peer_access_status(const char *call, int hip_error, const char *hip_name,
+                                    int dev_a, int dev_b, char *msg, size_t cap)
+{
+    if (hip_error == (int)hipSuccess || hip_error == (int)hipErrorPeerAccessAlreadyEnabled) {
+        if (msg && cap) msg[0] = '\0';
+        return GOL_OK;
+    }
+    if (msg && cap)
+        snprintf(msg, cap, "%s(%d -> %d) failed: %s (%d): the strips on devices %d and %d "
+                 "cannot exchange halos by peer copies", call ? call : "peer access", dev_a, dev_b,
+                 hip_name ? hip_name : "?", hip_error, dev_a, dev_b);
+    return GOL_EHIP;
+}
+
 const char *gol_run_error(gol_run *r)
 {
-    if (!r) return "";
+    if (!r) return t_start_error.c_str();
     std::lock_guard<std::mutex> lk(r->mu);
     return r->error.c_str();
 }

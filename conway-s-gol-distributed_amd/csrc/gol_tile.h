@@ -31,7 +31,16 @@
 // SEG and K.
 #pragma once
 #include "gol_device.h"
-#include "gol_tile_turn.h"
+#if GOL_TOOLS
+#include "gol_tile_turn.h"   // (ORD 8 / 9's generated inline-asm turns: tools build only)
+#else
+namespace golk {
+// (declared only: ORD 8 / 9 are instantiated in the tools build alone)
+template <int SEG, int V>
+__device__ __forceinline__ void tile_turn_asm(uint32_t (&v)[SEG][2], uint32_t (&ad)[4], uint32_t ps,
+                                              uint32_t ba);
+}  // namespace golk
+#endif
 
 #include <type_traits>
 

@@ -254,7 +254,11 @@ def Run(p: Params, events: Channel, keyPresses: Optional[Channel] = None, *,
     opts.engine_flags = N.GOL_FLAG_COUNT_EVERY_TURN if count_every_turn else 0
     opts.resume = -1 if resume is None else (1 if resume else 0)
     h = ctypes.c_void_p()
-    N.check(L.gol_run_start(ctypes.byref(prm), ctypes.byref(opts), ctypes.byref(h)))
+    rc = L.gol_run_start(ctypes.byref(prm), ctypes.byref(opts), ctypes.byref(h))
+    if rc < 0:
+        detail = L.gol_run_error(None)          # the start's own reason (e.g. peer access)
+        msg = L.gol_strerror(rc).decode()
+        raise N.GolError(rc, msg + (": " + detail.decode() if detail else ""))
     handle = RunHandle(h, L)
     done = threading.Event()
 

@@ -144,13 +144,65 @@ class DistStrip:
         self.stage_on_host = stage_on_host
         self.exchanges = 0
         self._layout_checked = False
+        self._stale = False            # start_window(): the next step exchanges first
+        self._ev_pool = []             # time_exchanges(): HIP event pairs not yet used
+        self._ev_used = []
+
+    def start_window(self):
+        """Make the next ``step`` begin with an exchange, whatever turns its halos have left:
+        a timed region that starts here holds exactly one exchange per ``halo`` turns (the
+        run's cadence), not a partial window left over from the warm-up.  (An exchange is
+        valid at any turn: the neighbours' owned rows are exact.)"""
+        self._stale = True
+
+    def time_exchanges(self, n: int):
+        """Bracket each of the next ``n`` exchanges with a HIP event pair on the stream the
+        transport runs on (created and recorded once here, so the timed region only records
+        them): ``exchange_us()`` then gives each exchange's duration -- the transfer plus
+        any wait for the neighbours, as the stream saw it."""
+        stream = getattr(self.strip, "stream", None)
+        if stream is None:
+            return
+        self._ev_pool, self._ev_used = [], []
+        for _ in range(int(n)):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            b.record(stream)
+            self._ev_pool.append((a, b))
+        stream.synchronize()
+
+    def exchange_us(self):
+        """Durations (us) of the exchanges timed since ``time_exchanges`` (synchronises)."""
+        if not self._ev_used:
+            return []
+        self._ev_used[-1][1].synchronize()
+        return [a.elapsed_time(b) * 1e3 for a, b in self._ev_used]
+
+    def _ev_begin(self, stream):
+        if not self._ev_pool:
+            return None
+        pair = self._ev_pool.pop()
+        pair[0].record(stream)
+        return pair
+
+    def _ev_end(self, pair, stream):
+        if pair is not None:
+            pair[1].record(stream)
+            self._ev_used.append(pair)
 
     def exchange(self):
+        self._stale = False
+        stream = getattr(self.strip, "stream", None)
+        pair = self._ev_begin(stream) if stream is not None else None
         ctx = getattr(self.strip, "stream_context", None)
         if ctx is None:
-            return self._exchange()
-        with ctx():
-            return self._exchange()
+            self._exchange()
+        else:
+            with ctx():
+                self._exchange()
+        if stream is not None:
+            self._ev_end(pair, stream)
 
     def _check_layout(self, like):
         """Zero-copy messages carry the engines' stepping layout: every rank must agree
@@ -210,16 +262,19 @@ class DistStrip:
         cs = self.comm_stream.cuda_stream
         eng.stream_wait(cs)                     # the send rows are final
         nbytes = top.numel() * top.element_size()
+        pair = self._ev_begin(self.comm_stream)
         self.rccl.exchange([(top.data_ptr(), self.up), (bot.data_ptr(), self.down)],
                            [(bot_recv.data_ptr(), self.down), (top_recv.data_ptr(), self.up)],
                            nbytes, cs)
+        self._ev_end(pair, self.comm_stream)
         self.strip.step_overlap(turns, cs)
+        self._stale = False
         self.exchanges += 1
 
     def step(self, turns: int):
         turns = int(turns)
         while turns > 0:
-            if self.strip.halo_valid == 0:
+            if self.strip.halo_valid == 0 or self._stale:
                 if self.overlap:
                     n = min(turns, self.strip.engine.halo)
                     self._exchange_overlapped(n)

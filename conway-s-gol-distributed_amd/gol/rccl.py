@@ -12,19 +12,66 @@ stream, ordered by the stream itself.
 The library is the RCCL that torch already loaded (``torch/lib/librccl.so``), so there is
 one RCCL in the process.  The communicator is our own: rank 0's ``ncclGetUniqueId`` is
 broadcast over the existing torch.distributed group (a 128-byte tensor) and every rank
-calls ``ncclCommInitRank``.  It replaces the reference's per-turn net/rpc strip transfer
+calls ``ncclCommInitRankConfig``.  It replaces the reference's per-turn net/rpc strip transfer
 (``Server/gol/distributor.go:185-224``).
+
+The communicator is created non-blocking (``ncclConfig_t.blocking = 0``) and its state polled
+against a deadline (``GOL_RCCL_INIT_TIMEOUT_S``, default 60 s): a bootstrap that cannot connect
+(a wrong root address, a rank that never arrives) aborts the communicator and raises
+``RcclTimeout`` on every rank within the deadline instead of hanging the job -- the reference
+Server's dial-or-fatal (``Server/gol/distributor.go:87-97``).  Only this communicator is
+non-blocking; torch's own keep their configuration.
 """
 from __future__ import annotations
 
 import ctypes
 import os
+import threading
+import time
 
 import torch
 import torch.distributed as dist
 
 NCCL_INT8 = 0                       # ncclInt8 (messages are raw packed words, sent as bytes)
+NCCL_IN_PROGRESS = 7                # ncclInProgress (a non-blocking communicator's pending state)
 _UID_BYTES = 128                    # NCCL_UNIQUE_ID_BYTES
+_CONFIG_MAGIC = 0xCAFEBEEF
+_UNDEF_INT = -2147483648            # NCCL_CONFIG_UNDEF_INT (INT_MIN)
+
+
+class RcclTimeout(RuntimeError):
+    """The communicator did not come up (or a group did not complete) within the deadline;
+    the communicator was aborted.  Not a reason to fall back to another transport: the peer
+    ranks are unreachable for that one too."""
+
+
+class _Config(ctypes.Structure):
+    """The leading fields of ncclConfig_t (NCCL 2.17 layout, ``size`` = this struct's size):
+    the library copies ``size`` bytes and keeps its defaults for the fields after them."""
+    _fields_ = [("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
+                ("blocking", ctypes.c_int), ("cgaClusterSize", ctypes.c_int),
+                ("minCTAs", ctypes.c_int), ("maxCTAs", ctypes.c_int),
+                ("netName", ctypes.c_char_p), ("splitShare", ctypes.c_int)]
+
+
+def nonblocking_config(version: int) -> _Config:
+    """NCCL_CONFIG_INITIALIZER with blocking = 0 (the library's own version in ``version``)."""
+    c = _Config()
+    c.size = ctypes.sizeof(_Config)
+    c.magic = _CONFIG_MAGIC
+    c.version = int(version)
+    c.blocking = 0
+    c.cgaClusterSize = c.minCTAs = c.maxCTAs = c.splitShare = _UNDEF_INT
+    c.netName = None
+    return c
+
+
+def init_timeout_s() -> float:
+    v = os.environ.get("GOL_RCCL_INIT_TIMEOUT_S", "")
+    try:
+        return max(1.0, float(v)) if v else 60.0
+    except ValueError:
+        return 60.0
 
 
 class _UniqueId(ctypes.Structure):
@@ -71,6 +118,10 @@ def lib() -> ctypes.CDLL:
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         L.ncclGetUniqueId.argtypes = [ctypes.POINTER(_UniqueId)]
         L.ncclCommInitRank.argtypes = [ctypes.POINTER(vp), i32, _UniqueId, i32]
+        L.ncclCommInitRankConfig.argtypes = [ctypes.POINTER(vp), i32, _UniqueId, i32,
+                                             ctypes.POINTER(_Config)]
+        L.ncclCommGetAsyncError.argtypes = [vp, ctypes.POINTER(i32)]
+        L.ncclCommAbort.argtypes = [vp]
         L.ncclCommDestroy.argtypes = [vp]
         L.ncclSend.argtypes = [vp, sz, i32, i32, vp, vp]
         L.ncclRecv.argtypes = [vp, sz, i32, i32, vp, vp]
@@ -79,7 +130,8 @@ def lib() -> ctypes.CDLL:
         L.ncclGetErrorString.argtypes = [i32]
         L.ncclGetErrorString.restype = ctypes.c_char_p
         L.ncclGetVersion.argtypes = [ctypes.POINTER(i32)]
-        for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclSend",
+        for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommInitRankConfig",
+                  "ncclCommGetAsyncError", "ncclCommAbort", "ncclCommDestroy", "ncclSend",
                   "ncclRecv", "ncclGroupStart", "ncclGroupEnd", "ncclGetVersion"):
             getattr(L, f).restype = i32
         _lib = L
@@ -102,7 +154,10 @@ class RcclComm:
     """One RCCL communicator over the ranks of ``group`` (collective constructor: every
     rank must create it, with its HIP device current)."""
 
-    def __init__(self, rank: int, world: int, device: torch.device, group=None):
+    def __init__(self, rank: int, world: int, device: torch.device, group=None,
+                 uid_hook=None):
+        """``uid_hook`` (tests only): a function applied to this rank's copy of the unique
+        id's bytes after the broadcast -- e.g. a wrong root port, to exercise the deadline."""
         self.rank, self.world = int(rank), int(world)
         self.comm = ctypes.c_void_p()
         uid = _UniqueId()
@@ -124,11 +179,53 @@ class RcclComm:
                 raise RuntimeError(f"rank {self.rank}: direct RCCL unavailable on some rank"
                                    + (f" ({err})" if err else ""))
             uid = broadcast_unique_id(uid, group, where)
+            if uid_hook is not None:
+                uid = uid_from_bytes(uid_hook(uid_to_bytes(uid)))
         elif err is not None:
             raise RuntimeError(f"direct RCCL unavailable ({err})")
+        self.timeout_s = init_timeout_s()
+        cfg = nonblocking_config(version())
+        t0 = time.monotonic()
         with torch.cuda.device(device):
-            _check(L.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),
-                   "ncclCommInitRank")
+            rc = L.ncclCommInitRankConfig(ctypes.byref(self.comm), self.world, uid, self.rank,
+                                          ctypes.byref(cfg))
+            if rc not in (0, NCCL_IN_PROGRESS):
+                self._abort()
+                _check(rc, "ncclCommInitRankConfig")
+            self._wait("ncclCommInitRankConfig", t0)
+        self.init_s = time.monotonic() - t0
+
+    def _state(self) -> int:
+        st = ctypes.c_int(0)
+        rc = lib().ncclCommGetAsyncError(self.comm, ctypes.byref(st))
+        return rc if rc != 0 else int(st.value)
+
+    def _abort(self):
+        """ncclCommAbort on a helper thread, given 10 s: an abort that itself hangs must not
+        keep the caller from failing."""
+        if not self.comm:
+            return
+        comm, self.comm = self.comm, ctypes.c_void_p()
+        th = threading.Thread(target=lambda: lib().ncclCommAbort(comm), daemon=True)
+        th.start()
+        th.join(10.0)
+
+    def _wait(self, what: str, t0: float):
+        """Poll the communicator until its pending operation is done; abort and raise
+        RcclTimeout past the deadline, RuntimeError on an RCCL error."""
+        while True:
+            st = self._state()
+            if st == 0:
+                return
+            if st != NCCL_IN_PROGRESS:
+                self._abort()
+                _check(st, what)
+            if time.monotonic() - t0 > self.timeout_s:
+                self._abort()
+                raise RcclTimeout(f"rank {self.rank}: {what} did not complete within "
+                                  f"{self.timeout_s:g} s (GOL_RCCL_INIT_TIMEOUT_S); communicator "
+                                  f"aborted")
+            time.sleep(0.0005)
 
     def exchange(self, sends, recvs, nbytes: int, stream_ptr: int):
         """One group of point-to-point ops on ``stream_ptr``: ``sends`` / ``recvs`` are
@@ -145,7 +242,14 @@ class RcclComm:
                 _check(L.ncclRecv(ctypes.c_void_p(rp), nbytes, NCCL_INT8, int(rpeer),
                                   self.comm, s), "ncclRecv")
         finally:
-            _check(L.ncclGroupEnd(), "ncclGroupEnd")
+            rc = L.ncclGroupEnd()
+        if rc == NCCL_IN_PROGRESS:
+            # (non-blocking communicator: the first group also connects the peers; the ops are
+            # on the stream once the state is ncclSuccess, so the caller's next launch on the
+            # same stream is ordered after them)
+            self._wait("ncclGroupEnd", time.monotonic())
+        else:
+            _check(rc, "ncclGroupEnd")
 
     def close(self):
         if self.comm:

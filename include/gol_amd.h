@@ -310,7 +310,9 @@ int gol_run_next_event(gol_run *r, gol_event *ev, int32_t timeout_ms);
 int64_t gol_run_final_alive(gol_run *r, int64_t *xy, int64_t cap);
 /* keyPresses <- rune ('s', 'p', 'q', 'k'). */
 int gol_run_key(gol_run *r, int32_t rune);
-/* Error text of a run that failed (the events channel is closed early). */
+/* Error text of a run that failed (the events channel is closed early).  NULL: why the calling
+ * thread's last gol_run_start failed after validating its arguments (e.g. GOL_EHIP: two strip
+ * devices that report peer access but refuse to enable it); "" after a successful start. */
 const char *gol_run_error(gol_run *r);
 /* Join the driver thread and free the run. */
 void gol_run_destroy(gol_run *r);

@@ -112,6 +112,36 @@ def test_strerror_and_no_device_paths():
         assert L.gol_create(64, 64, 0, ctypes.byref(h)) == N.GOL_ENODEV
 
 
+def test_peer_access_error_mapping():
+    """Round-5 verdict #6: gol_run_start maps each peer-access call between two strips'
+    devices through gol_internal_peer_access_status (gol_run.cpp; pure, no HIP call): success
+    and hipErrorPeerAccessAlreadyEnabled (704) start the run, anything else fails it with
+    GOL_EHIP and a message naming the call, the HIP error and the device pair (returned by
+    gol_run_error(NULL))."""
+    from gol import _native as N
+    L = N.lib()
+    f = L.gol_internal_peer_access_status
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_char_p, ctypes.c_size_t]
+    buf = ctypes.create_string_buffer(256)
+    assert f(b"hipDeviceEnablePeerAccess", 0, b"hipSuccess", 0, 1, buf, 256) == N.GOL_OK
+    assert buf.value == b""
+    assert f(b"hipDeviceEnablePeerAccess", 704, b"hipErrorPeerAccessAlreadyEnabled", 2, 3,
+             buf, 256) == N.GOL_OK
+    rc = f(b"hipDeviceEnablePeerAccess", 217, b"hipErrorPeerAccessUnsupported", 0, 5, buf, 256)
+    assert rc == N.GOL_EHIP
+    msg = buf.value.decode()
+    assert msg.startswith("hipDeviceEnablePeerAccess(0 -> 5) failed: "
+                          "hipErrorPeerAccessUnsupported (217)"), msg
+    assert "devices 0 and 5" in msg
+    assert f(b"hipDeviceCanAccessPeer", 101, b"hipErrorInvalidDevice", 1, 9, buf, 16) == N.GOL_EHIP
+    assert len(buf.value) == 15                          # truncated to the buffer, NUL-ended
+    # no failed start on this thread yet: gol_run_error(NULL) is empty
+    L.gol_run_error.restype = ctypes.c_char_p
+    assert L.gol_run_error(None) == b""
+
+
 def test_struct_layouts_match_header():
     """ctypes mirrors of the header structs have the C sizes (compiled probe)."""
     from gol import _native as N

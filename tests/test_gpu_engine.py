@@ -523,7 +523,8 @@ def test_driver_command_digest(gol, monkeypatch, pin):
     """The driver's bench command at the headline size (bench.py --steps 20 --warmup 5):
     65536^2 seed 3, one gol_step of 5 turns, then one of 20, against the oracle digest of 25
     turns -- with the engine's own choice (the pinned MI355X shape: one k_step_tile launch of
-    20 turns on 30 x 336 tiles of ORD 5 SEG 24, code 524, the launch BENCH_r04 timed), with
+    20 turns on 30 x 336 tiles of ORD 5 SEG 24, code 524, the launch the driver's bench line
+    times), with
     that launch forced through GOL_TILE, and with the create-time search (GOL_AUTOTUNE=2)."""
     if pin == "tile":
         monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
@@ -584,9 +585,10 @@ PINNED_STRIP_SHAPES = {8: (16, 352, 14, 112), 4: (32, 704, 14, 524), 2: (32, 704
 def test_pinned_shape_digest(gol, key):
     """Each BASELINE board size runs its pinned shape (no create-time search: the kernel the
     bench times is the one profiles/ measured, on every box) and matches the oracle's
-    full-size digest: 65536^2 x 1000 (configs[3], 50 launches of K = 20), 16384^2 x 10000
-    (configs[2], K = 32 on 14 x 316 tiles of ORD 1 SEG 6), 5120^2 x 1000 (configs[1], K = 32
-    on 14 x 128 tiles of ORD 2 SEG 3)."""
+    full-size digest -- the shapes of PINNED_SHAPES: 65536^2 x 1000 (configs[3], K = 24 on
+    30 x 336 tiles of ORD 5 SEG 24: 34 x 24 + 8 x 23 turns), 16384^2 x 10000 (configs[2], K =
+    32 on 14 x 320 tiles of ORD 1 SEG 12), 5120^2 x 1000 (configs[1], K = 32 on 14 x 128 tiles
+    of ORD 2 SEG 3)."""
     d = _digests()[key]
     K, th, tw, code = PINNED_SHAPES[d["width"]]
     with _engine(gol, d["width"], d["height"]) as e:
@@ -601,6 +603,25 @@ def test_pinned_shape_digest(gol, key):
         assert {(t[0], t[1]) for t in tiles} == {(tw, code)}
         assert e.snapshot() == (d["turns"], d["alive"])
         assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
+
+
+def test_pinned_check_runs_once_per_shape(gol, monkeypatch):
+    """Round-5 verdict #5 / advice (medium): a pinned shape is applied whatever its create-time
+    timing says (the check only warns), and the check runs once per (device, width, buffer
+    rows) per process -- a second engine of the same pinned size is created in < 5 ms.  (A
+    3000 ms budget makes a first check unmistakable; 5120^2 is pinned.)"""
+    import time
+    monkeypatch.setenv("GOL_PIN_VERIFY_MS", "3000")
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        e = gol.Engine(5120, 5120, device=0)
+        times.append((time.perf_counter() - t0) * 1e3)
+        assert e.info().shape_source == 2
+        e.close()
+    # the first engine of the shape in this process may have run the check (unless an earlier
+    # test created a 5120^2 engine); the later ones never do
+    assert times[1] < 5.0 and times[2] < 5.0, times
 
 
 def test_65536_properties(gol, oracle):

@@ -4,9 +4,15 @@ broadcast over a gloo group.  RCCL refuses two ranks on one device ("Duplicate G
 detected", ncclInvalidUsage = 5), but only after its bootstrap has connected every rank to
 the root address carried in the unique id -- so INIT_DUP (or INIT_OK, should RCCL accept the
 pair) proves the id arrived intact; a damaged id fails earlier, in the bootstrap's connect
-(a system or remote error)."""
+(a system or remote error).
+
+--bad-port: rank 1 alters the root port in its copy of the id, so it can never join.  The
+communicator's non-blocking init is polled against GOL_RCCL_INIT_TIMEOUT_S: rank 0 (the root,
+waiting for rank 1) must report INIT_TIMEOUT, rank 1 INIT_TIMEOUT or INIT_FAIL, both within
+the deadline plus the abort's grace, instead of hanging."""
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "conway-s-gol-distributed_amd"))
@@ -14,23 +20,38 @@ sys.path.insert(0, os.path.join(ROOT, "conway-s-gol-distributed_amd"))
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from gol.rccl import RcclComm  # noqa: E402
+from gol.rccl import RcclComm, RcclTimeout  # noqa: E402
+
+
+def bad_port(uid: bytes) -> bytes:
+    """The id with its root port (bytes 10-11: the sockaddr after the 8-byte magic and the
+    2-byte family) changed."""
+    return uid[:10] + bytes([uid[10] ^ 0x5A, uid[11] ^ 0x3C]) + uid[12:]
 
 
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
     torch.cuda.set_device(0)
+    hook = bad_port if "--bad-port" in sys.argv[1:] and rank == 1 else None
+    t0 = time.monotonic()
     try:
-        c = RcclComm(rank, world, torch.device("cuda", 0))
+        c = RcclComm(rank, world, torch.device("cuda", 0), uid_hook=hook)
         c.close()
         print(f"rank {rank}: INIT_OK", flush=True)
+    except RcclTimeout as e:
+        print(f"rank {rank}: INIT_TIMEOUT after {time.monotonic() - t0:.1f} s: {e}", flush=True)
     except RuntimeError as e:
         msg = str(e)
         tag = "INIT_DUP" if "RCCL error 5" in msg else "INIT_FAIL"
-        print(f"rank {rank}: {tag} {msg}", flush=True)
+        print(f"rank {rank}: {tag} after {time.monotonic() - t0:.1f} s: {msg}", flush=True)
     dist.barrier()
     dist.destroy_process_group()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    # (an aborted communicator may leave RCCL helper threads behind: end the process here
+    # rather than in the interpreter's shutdown)
+    os._exit(0)
 
 
 if __name__ == "__main__":
