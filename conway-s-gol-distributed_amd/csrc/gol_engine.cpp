@@ -998,6 +998,19 @@ constexpr KnownShape kKnownShapes[] = {
     {65536, 8448, {16, 352, 14, 112, 0}, 5.3f},
     {65536, 16640, {32, 704, 14, 524, 0}, 9.5f},
     {65536, 33024, {32, 704, 14, 524, 0}, 18.4f},
+    // configs[3..4] as row strips with the bench's default halo for its 20-turn command
+    // (min(128, turns): 20 rows, one exchange and one 20-turn launch per window; buffer = H / N
+    // + 40 rows): ORD 1 SEG 12 (west carry) on 14 x 344 tiles, K = 20, the fastest of 30-44
+    // shapes at every N (N = 8 / 4 / 2: 4.95 / 9.28 / 18.16 us per turn; ORD 5 SEG 12 5.11 /
+    // -, ORD 5 SEG 24 5.29 / 9.44 / 18.29; profiles/r06_strip_sweep.log)
+    {65536, 8232, {20, 344, 14, 112, 0}, 4.95f},
+    {65536, 16424, {20, 344, 14, 112, 0}, 9.28f},
+    {65536, 32808, {20, 344, 14, 112, 0}, 18.16f},
+    // configs[2] on 2 GPUs: 16384^2 as 2 strips with 128-row halos (16384 x 8448): ORD 5 SEG 12
+    // on 30 x 320 tiles, K = 32, 16-wave workgroups: 1.72 us per turn (30 x 320 ORD 1 SEG 12
+    // 1.73, 14 x 704 ORD 5 SEG 12 1.74, the 14 x 320 ORD 1 torus pin slower;
+    // profiles/r06_strip_sweep.log)
+    {16384, 8448, {32, 320, 30, 512, 0}, 1.72f},
 };
 
 bool known_shape(const gol_ctx *c, KnownShape *out)

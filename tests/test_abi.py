@@ -193,7 +193,7 @@ def test_pinned_shapes_match_the_tests():
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import test_gpu_engine as T
     want = {(s, s): v for s, v in T.PINNED_SHAPES.items()}
-    want.update({(65536, 65536 // n + 256): v for n, v in T.PINNED_STRIP_SHAPES.items()})
+    want.update(T.PINNED_STRIP_SHAPES)
     assert got == want
     assert all(v[3] in TILE_CODES for v in got.values())
 

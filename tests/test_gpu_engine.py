@@ -576,8 +576,15 @@ def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key, code):
 # width in lanes, segment code); the bench's configs run exactly these, and profiles/ has a
 # kernel-trace + PMC summary of each
 PINNED_SHAPES = {65536: (24, 336, 30, 524), 16384: (32, 320, 14, 112), 5120: (32, 128, 14, 203)}
-# ... and for 65536^2 as N row strips with 128-row halos
-PINNED_STRIP_SHAPES = {8: (16, 352, 14, 112), 4: (32, 704, 14, 524), 2: (32, 704, 14, 524)}
+# ... and for row strips, by (board width, buffer rows = owned rows + 2 x halo): 65536^2 as N
+# strips with 128-row halos and with the bench's 20-row halos for its 20-turn command, and
+# 16384^2 as 2 strips with 128-row halos (configs[2] on 2 GPUs)
+PINNED_STRIP_SHAPES = {
+    (65536, 8448): (16, 352, 14, 112), (65536, 16640): (32, 704, 14, 524),
+    (65536, 33024): (32, 704, 14, 524),
+    (65536, 8232): (20, 344, 14, 112), (65536, 16424): (20, 344, 14, 112),
+    (65536, 32808): (20, 344, 14, 112),
+    (16384, 8448): (32, 320, 30, 512)}
 
 
 @pytest.mark.parametrize("key", ["65536x65536_seed3_t1000", "16384x16384_seed2_t10000",
@@ -643,14 +650,11 @@ def test_65536_properties(gol, oracle):
 
 
 # ------------------------------------------------- full-size strip forms (C4 / C5)
-@pytest.mark.parametrize("n", [2, 4, 8])
-def test_65536_strips_in_process(gol, n):
-    """BASELINE configs C4 / C5 in strip form at full size on one GPU: 65536^2 seed 3 as
-    n row strips (the reference Server's split, Server/gol/distributor.go:106-116), each
-    its own engine with 128-row halos exchanged every 128 turns (temporal blocking inside:
-    k-turn launches, k-row shrinking trapezoids), 1000 turns, against the oracle digest."""
-    d = _digests()["65536x65536_seed3_t1000"]
-    w, h, turns, K = d["width"], d["height"], d["turns"], 128
+def _run_strips_in_process(gol, d, n, K):
+    """d's board as n row strips (the reference Server's split, Server/gol/distributor.go:
+    106-116), each its own engine with K-row halos exchanged every K turns by peer copies;
+    returns (engines' infos, the strips' tile shapes, alive, sha256 of the packed board)."""
+    w, h, turns = d["width"], d["height"], d["turns"]
     parts = gol.strip_split(h, n)
     engs = [gol.Engine(w, h, device=0, row_offset=o, rows=r, halo=K) for o, r in parts]
     try:
@@ -668,22 +672,51 @@ def test_65536_strips_in_process(gol, n):
             for e in engs:
                 e.step(m)
             left -= m
-        assert all(e.info().turns_per_launch > 1 for e in engs)
-        # the strips run their pinned MI355X shape (gol_engine.cpp kKnownShapes), the shape the
-        # N-GPU bench times on every rank
-        K_, th, tw, code = PINNED_STRIP_SHAPES[n]
-        for e in engs:
-            i = e.info()
-            assert (i.shape_source, i.turns_per_launch, i.band_rows) == (2, K_, th), n
-            assert {(t[0], t[1]) for t in e.last_launch_tiles(blocks=True)} == {(tw, code)}
-        assert sum(e.snapshot()[1] for e in engs) == d["alive"]
+        infos = [e.info() for e in engs]
+        tiles = [{(t[0], t[1]) for t in e.last_launch_tiles(blocks=True)} for e in engs]
+        alive = sum(e.snapshot()[1] for e in engs)
         hs = hashlib.sha256()
         for e in engs:
             hs.update(e.read_packed().tobytes())
-        assert hs.hexdigest() == d["sha256"]
+        return infos, tiles, alive, hs.hexdigest()
     finally:
         for e in engs:
             e.close()
+
+
+@pytest.mark.parametrize("n,K", [(2, 128), (4, 128), (8, 128), (2, 20), (4, 20), (8, 20)])
+def test_65536_strips_in_process(gol, n, K):
+    """BASELINE configs C4 / C5 in strip form at full size on one GPU: 65536^2 seed 3 as
+    n row strips, each its own engine with K-row halos exchanged every K turns (temporal
+    blocking inside: k-turn launches, k-row shrinking trapezoids), 1000 turns, against the
+    oracle digest.  K = 128: the bench's halo for long runs; K = 20: its halo for the
+    driver's 20-turn command (one exchange and one 20-turn launch per window, C5's "k-row
+    halos every k turns")."""
+    d = _digests()["65536x65536_seed3_t1000"]
+    infos, tiles, alive, sha = _run_strips_in_process(gol, d, n, K)
+    assert all(i.turns_per_launch > 1 for i in infos)
+    # the strips run their pinned MI355X shape (gol_engine.cpp kKnownShapes), the shape the
+    # N-GPU bench times on every rank
+    K_, th, tw, code = PINNED_STRIP_SHAPES[(65536, 65536 // n + 2 * K)]
+    for i, t in zip(infos, tiles):
+        assert (i.shape_source, i.turns_per_launch, i.band_rows) == (2, K_, th), n
+        assert t == {(tw, code)}
+    assert alive == d["alive"]
+    assert sha == d["sha256"]
+
+
+def test_16384_two_strips_in_process(gol):
+    """BASELINE configs[2] on 2 GPUs, in strip form on one GPU: 16384^2 seed 2 as 2 row strips
+    with 128-row halos (79 exchanges), 10000 turns, on the pinned 16384 x 8448 strip shape (the
+    one the 2-GPU bench times, profiled in profiles/), against the oracle digest."""
+    d = _digests()["16384x16384_seed2_t10000"]
+    infos, tiles, alive, sha = _run_strips_in_process(gol, d, 2, 128)
+    K_, th, tw, code = PINNED_STRIP_SHAPES[(16384, 8448)]
+    for i, t in zip(infos, tiles):
+        assert (i.shape_source, i.turns_per_launch, i.band_rows, i.buffer_rows) == (2, K_, th, 8448)
+        assert t == {(tw, code)}
+    assert alive == d["alive"]
+    assert sha == d["sha256"]
 
 
 # ---------------------------------------------------------------- control word

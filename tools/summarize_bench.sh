@@ -5,7 +5,7 @@
 # and the headline alternates (h2.., pinned passes only).
 set -eu
 R="$(cd "$(dirname "$0")/.." && pwd)"
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 O="$R/gpurun_out/prof_$ROUND"
 board_of() { case $1 in h) echo 0;; c3) echo 1;; c2) echo 2;; *) echo -;; esac; }
 while read -r name size k shape args; do
@@ -16,4 +16,4 @@ while read -r name size k shape args; do
   python3 "$R/tools/summarize_profile.py" "${ROUND}_k${k}_${size}_${name}" "$O" "$kt" \
     "fetch_$name" "write_$name" "$b" "$kn" "$shape" "sq_$name" "ktpin_$name" > /dev/null
   echo "${ROUND}_k${k}_${size}_${name}"
-done < "$O/pins.txt"
+done < "$O/${PINS:-pins.txt}"

@@ -128,9 +128,10 @@ def main(tag, src, kt, fetch=None, write=None, board="0", kernel=None, shape=Non
         us = statistics.median(list(dur.values())[-20:])
         res["sq_counters_median"] = med
         res["sq_dispatch_us_median"] = us
-        if "GRBM_GUI_ACTIVE" in med and us >= 100:
+        if "GRBM_GUI_ACTIVE" in med and us >= 90:
             # (GRBM_GUI_ACTIVE spans more than a short dispatch: 5120^2's 17 us launches read
-            # 3.3 GHz, above the 2.4 GHz maximum; no clock from dispatches under 100 us)
+            # 3.3 GHz, above the 2.4 GHz maximum; no clock from dispatches under 90 us -- the
+            # N = 8 strip's 20-turn launch takes ~99)
             res["clock_ghz"] = round(med["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3), 4)
         if "SQ_ACTIVE_INST_VALU" in med and "SQ_WAVE_CYCLES" in med:
             res["valu_active_per_wave_cycle"] = round(med["SQ_ACTIVE_INST_VALU"] /
