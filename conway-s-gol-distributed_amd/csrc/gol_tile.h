@@ -66,6 +66,15 @@ __device__ __forceinline__ void tile_turn_asm(uint32_t (&v)[SEG][2], uint32_t (&
 #ifndef GOL_TILE_WEST_CARRY
 #define GOL_TILE_WEST_CARRY 1
 #endif
+// Raw edge rows (ORD 0-2, one word per lane, segments of up to GOL_TILE_RAW rows; 0 = never):
+// each lane publishes its first and last row as they are -- one 16-B LDS slot, one
+// ds_write_b128 -- instead of their two 3-cell row sums (two slots, two ds_write_b128), and
+// sums the rows it reads from the segments above and below itself (two more row sums a turn).
+// Half the LDS bytes per turn for 8 more VALU per neighbour row: the trade pays where a turn's
+// LDS stores, not its VALU, are the critical path -- short segments on small boards.
+#ifndef GOL_TILE_RAW
+#define GOL_TILE_RAW 0
+#endif
 template <int SEG, int W>
 constexpr bool tile_west_carry() { return GOL_TILE_WEST_CARRY && W == 1 && SEG >= 4 && SEG <= 16; }
 
@@ -268,6 +277,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     // profiles/r03_tile_unroll_ab.log).  The threshold 12: pairs at SEG 8 are 2-3 % faster
     // than one body, at SEG 16 11-28 % slower (profiles/r03b_tile_pairs_threshold.log).
     constexpr bool kPairs = SEG * W <= GOL_TILE_PAIRS_MAX;
+    constexpr bool kRaw = ORD < 4 && W == 1 && SEG <= GOL_TILE_RAW;
     // (with pairs the lane's four LDS addresses of each parity are loop-invariant registers;
     // one body forms them per turn -- precomputed there, the long bodies ran 4-8 % slower)
     uint4 *const wtop2[2] = {xsh + o_wt, xsh + 2 * nslot + o_wt};
@@ -391,17 +401,35 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         constexpr int p = decltype(P)::value;
         const int off = poff;
         // the segment's first and last row sums go to the neighbours (row sums, not rows: no
-        // lane sums a row twice -- SEG row sums and SEG rules per turn)
+        // lane sums a row twice -- SEG row sums and SEG rules per turn); kRaw: the rows
         uint32_t F[NS], Lr[NS];
         rsum(v[0], F);
         rsum(v[SEG - 1], Lr);
-        put(wtop(p, off), F);
-        put(wbot(p, off), Lr);
+        if constexpr (kRaw) {
+            *wtop(p, off) = make_uint4(v[0][0], v[0][1], v[SEG - 1][0], v[SEG - 1][1]);
+        } else {
+            put(wtop(p, off), F);
+            put(wbot(p, off), Lr);
+        }
         uint32_t U[NS], D[NS];
+        // kRaw: the last row of the segment above (the z, w half of its slot) and the first
+        // row of the one below (x, y), summed here
+        auto get_raw = [&](uint32_t (&Us)[NS], uint32_t (&Ds)[NS]) {
+            const uint4 *const base = kPairs ? xsh + 2 * nslot * p : xsh + off;
+            const uint2 a = *(reinterpret_cast<const uint2 *>(base + s_up) + 1);
+            const uint2 b = *reinterpret_cast<const uint2 *>(base + s_dn);
+            const uint32_t ra[ND] = {a.x, a.y}, rb[ND] = {b.x, b.y};
+            rsum(ra, Us);
+            rsum(rb, Ds);
+        };
         if constexpr (ORD < 2 || ORD == 3) {
             if constexpr (ORD != 3) __syncthreads();   // ORD 3: timing ablation (tools build)
-            get(rup(p, off), U);
-            get(rdn(p, off), D);
+            if constexpr (kRaw) {
+                get_raw(U, D);
+            } else {
+                get(rup(p, off), U);
+                get(rdn(p, off), D);
+            }
         }
         if constexpr (ORD == 0 || ORD == 3) {
             // in order: A, B, Cs = sums of rows i-1, i, i+1
@@ -465,8 +493,12 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
                 // ORD 2: the barrier after the interior rows -- a wave that arrives early has
                 // already done all the work that needs no neighbour
                 __syncthreads();
-                get(rup(p, off), U);
-                get(rdn(p, off), D);
+                if constexpr (kRaw) {
+                    get_raw(U, D);
+                } else {
+                    get(rup(p, off), U);
+                    get(rdn(p, off), D);
+                }
             }
             rule(U, F, S1, v[0]);
             rule(Pw, Lr, D, v[SEG - 1]);

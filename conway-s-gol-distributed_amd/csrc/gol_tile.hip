@@ -105,9 +105,20 @@ static void *stream_fn(int code)
 #endif
 }
 
+// (A/B builds: make variant VDEFS=-DGOL_TILE_W2_SEG12=1 adds two words per lane at SEG 12,
+// ORD 1 and 5 -- codes 1112 and 1512 -- the round-5 verdict's candidate for fewer lane
+// shifts per word at the VGPRs of SEG 24 with one word)
+#ifndef GOL_TILE_W2_SEG12
+#define GOL_TILE_W2_SEG12 0
+#endif
+
 void *tile_kernel(int code)
 {
     const int seg = code % 100, ord = (code / 100) % 10, w = tile_seg_words(code);
+#if GOL_TILE_W2_SEG12
+    if (code == 1112) return reinterpret_cast<void *>(&k_step_tile<12, 1, 2>);
+    if (code == 1512) return reinterpret_cast<void *>(&k_step_tile<12, 5, 2>);
+#endif
 #if GOL_TOOLS   // ORD 3: no barrier between turns (wrong boards): what the turn's sync costs
     if (ord == 3 && w == 1) return tile_fn<3, 1>(seg);
 #endif
@@ -143,7 +154,9 @@ bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
 {
     if (turns < 2 || turns > 64 || tile_h < 1 || tile_w < 1 || tile_w + 2 > 64 || !tile_kernel(seg))
         return false;
-    if (!GOL_TOOLS && !tile_code_shipped(seg)) return false;   // (untested instantiations)
+    if (!GOL_TOOLS && !tile_code_shipped(seg) && !(GOL_TILE_W2_SEG12 && seg % 1000 == 112) &&
+        !(GOL_TILE_W2_SEG12 && seg % 1000 == 512))
+        return false;   // (untested instantiations)
     if (nw % tile_seg_words(seg)) return false;          // (whole word pairs per lane)
     const int C = tile_w + 2, G = 64 / C;
     const int ord = seg / 100 % 10;

@@ -21,8 +21,13 @@
  *              and at once while it is parked, so the ticker keeps firing while paused.  It
  *              ends on the unbuffered `done` channel (:59, :162-163, :198): main's send returns
  *              only once the ticker is back in its select, i.e. after any tick in flight has
- *              emitted its AliveCellsCount; main sends right after gol_step returns, so no
- *              AliveCellsCount follows FinalTurnComplete / StateChange Quitting.
+ *              emitted its AliveCellsCount.  Here main sends right after gol_step returns, so
+ *              no AliveCellsCount follows FinalTurnComplete / StateChange Quitting.  That order
+ *              is STRICTER than the reference, not a copy of it: distributor.go sends
+ *              FinalTurnComplete and Quitting (:194-195) before ticker.Stop and done <- true
+ *              (:197-198), so in the reference a tick that fires in between can still emit an
+ *              AliveCellsCount after Quitting.  Every event sequence this harness produces is
+ *              one the reference can produce.
  * GOL_HARNESS_TICK_DELAY_MS (tests): sleep between a tick's snapshot and its event, so a tick is
  * in flight when the run ends.
  *

@@ -445,7 +445,11 @@ def test_stub_harness_no_tick_after_quitting(workdir, monkeypatch):
     once the ticker is back in its select.  Here every tick sleeps 40 ms between its snapshot
     and its event while ticks come every 5 ms, so the run almost always ends with a tick in
     flight: its AliveCellsCount must still come before FinalTurnComplete, and none after
-    StateChange Quitting.  Every count is the oracle's at its turn."""
+    StateChange Quitting.  Every count is the oracle's at its turn.  (This order is stricter
+    than the reference's own: Local/gol/distributor.go sends FinalTurnComplete and Quitting
+    (:194-195) before ticker.Stop and done <- true (:197-198), so a tick in that gap can follow
+    Quitting there.  The stub ends the ticker first; its sequences are a subset of the
+    reference's.)"""
     monkeypatch.setenv("GOL_HARNESS_TICK_DELAY_MS", "40")
     series = G.alive_series(512)
     ticks_seen = 0
