@@ -1,6 +1,6 @@
 """bench.py takes `traffic` and the clock under load only from a committed profile summary
 whose launch shape equals the launch it timed.  CPU only: reads the
-committed profiles/r04_* / r05_* summaries."""
+committed profiles/r0[4-6]_* summaries."""
 import json
 import os
 import sys
@@ -16,18 +16,20 @@ def _bench():
 
 def test_summary_matches_shape_exactly():
     b = _bench()
-    d = json.load(open(os.path.join(ROOT, "profiles", "r04_k20_65536_h2_summary.json")))
+    d = json.load(open(os.path.join(ROOT, "profiles", "r06_k20_65536_h_summary.json")))
     got, src = b.pmc_summary(65536, 20, d["shape"])
-    # (the newest summary of that exact shape: round 5's pass of the pinned shape, or round 4's
-    # h / h2 of the same shape)
-    assert src.startswith((os.path.join("profiles", "r05_k20_65536_h"),
-                           os.path.join("profiles", "r04_k20_65536_h"))), src
+    # (the newest summary of that exact shape -- since round 6 a shape names its buffer rows,
+    # so a strip's summary never serves the torus of the same width and tile)
+    assert src == os.path.join("profiles", "r06_k20_65536_h_summary.json"), src
     assert got["shape"] == d["shape"]
     assert got["traffic_bytes_per_launch"] > 0 and 1.9 < got["clock_ghz"] < 2.5
     other = json.loads(json.dumps(d["shape"]))
     other["band_rows"] += 1
     other["tile"]["height_rows"] += 1
     assert b.pmc_summary(65536, 20, other) == (None, None)
+    strip = json.loads(json.dumps(d["shape"]))
+    strip["buffer_rows"] = 8232
+    assert b.pmc_summary(65536, 20, strip) == (None, None)
     traffic, src = b.pmc_traffic(65536, 20, d["shape"])
     assert traffic == got["traffic_bytes_per_launch"]
 
@@ -35,7 +37,7 @@ def test_summary_matches_shape_exactly():
 def test_every_r04_summary_has_one_kernel():
     """Each pinned pass measured one instantiation (its FETCH / WRITE kernel sets are one name)."""
     import glob
-    files = glob.glob(os.path.join(ROOT, "profiles", "r0[45]_k*_summary.json"))
+    files = glob.glob(os.path.join(ROOT, "profiles", "r0[456]_k*_summary.json"))
     assert len(files) >= 4
     for f in files:
         d = json.load(open(f))
@@ -43,19 +45,35 @@ def test_every_r04_summary_has_one_kernel():
         assert "shape" in d, f
 
 
+def _tile_shape(K, th, tw, code, rows):
+    seg = code % 100
+    G = 64 // (tw + 2)
+    waves = -(-(-(-(th + 2 * K) // seg)) // G)
+    return {"kernel": 15, "turns": K, "band_rows": th, "buffer_rows": rows,
+            "tile": {"code": code, "width_words": tw, "width_lanes": tw, "height_rows": th,
+                     "seg_rows": seg, "turn_order": code // 100 % 10, "words_per_lane": 1,
+                     "waves_per_workgroup": waves}}
+
+
 def test_pinned_shapes_have_profiles():
-    """Every BASELINE config the bench measures at N = 1 runs a pinned shape, and profiles/ holds a
-    PMC summary of exactly that shape, so `traffic` is never null (round-4 verdict item 2)."""
+    """Every pinned shape -- the BASELINE boards at N = 1 and the row strips the N > 1 bench
+    times -- has a PMC summary of exactly that launch (buffer rows included), with traffic and
+    an SQ pass, so `traffic`, `valu_inflation` and `valu_cycles_per_instr` are never null
+    (round-4 verdict item 2, round-5 verdict #1); the headline's 20-turn launch of the K = 24
+    torus shape has its own."""
     b = _bench()
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import test_gpu_engine as T
-    for size, (K, th, tw, code) in T.PINNED_SHAPES.items():
-        seg = code % 100
-        G = 64 // (tw + 2)
-        waves = -(-(-(-(th + 2 * K) // seg)) // G)
-        shape = {"kernel": 15, "turns": K, "band_rows": th,
-                 "tile": {"code": code, "width_words": tw, "width_lanes": tw, "height_rows": th,
-                          "seg_rows": seg, "turn_order": code // 100 % 10, "words_per_lane": 1,
-                          "waves_per_workgroup": waves}}
-        traffic, src = b.pmc_traffic(size, K, shape)
-        assert traffic and traffic > 0, (size, shape)
+    shapes = [(size, _tile_shape(K, th, tw, code, size))
+              for size, (K, th, tw, code) in T.PINNED_SHAPES.items()]
+    shapes += [(w, _tile_shape(K, th, tw, code, rows))
+               for (w, rows), (K, th, tw, code) in T.PINNED_STRIP_SHAPES.items()]
+    K, th, tw, code = T.PINNED_SHAPES[65536]
+    shapes.append((65536, _tile_shape(20, th, tw, code, 65536)))
+    for size, shape in shapes:
+        d, src = b.pmc_summary(size, shape["turns"], shape)
+        assert d and d["traffic_bytes_per_launch"] > 0, (size, shape)
+        assert d["sq_counters_median"]["SQ_INSTS_VALU"] > 0, src
+        # (against every buffer row: the passes ran a torus of the strip's buffer height)
+        cpi, infl = b.valu_figures(d, size * shape["buffer_rows"], shape["turns"])
+        assert infl and 1.0 < infl < 2.0, (src, infl)
