@@ -275,6 +275,13 @@ def measure(a, size, steps, warmup, world, rank, gpu, dev, dev_ids, stream, seed
     launches = info.launches - launches0
     exchanges = getattr(runner, "exchanges", 0) - exchanges0
     xus = runner.exchange_us() if world > 1 else []
+    if world > 1 and steps > eng.halo:
+        # the timed region's last gol_step ran only the last (partial) window: take the launch
+        # shape from one more whole window, untimed (every rank: it exchanges first)
+        runner.start_window()
+        runner.step(eng.halo)
+        plan = eng.last_launches()
+        tiles = eng.last_launch_tiles(blocks=True)
     comp = None
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64,
