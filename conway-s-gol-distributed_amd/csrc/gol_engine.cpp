@@ -979,10 +979,13 @@ struct KnownShape {
     float us_per_turn;                       // measured steady state (round-4 sweeps)
 };
 constexpr KnownShape kKnownShapes[] = {
-    // configs[3..4]: ORD 5, SEG 24, 8-wave workgroups (6 waves per SIMD); 34.0-34.7 us per turn
-    // (profiles/r04_sweep_65536_ord5.log, r04_sweep_65536_fine.log; K = 24 ~1 % ahead of K = 20,
-    // profiles/r05_ord7_ab.log); the driver's 20-turn call is one 20-turn launch of this shape
-    {65536, 65536, {24, 336, 30, 524, 0}, 34.0f},
+    // configs[3..4]: ORD 5, SEG 24 (6 waves per SIMD), K = 20 on 30 x 536 tiles in 12-wave
+    // workgroups (2 per CU): the driver's 20-turn call is one launch of exactly this depth,
+    // 117.8-120.1k GCUPS against 115.9-118.4k for round 5's K = 24 on 30 x 336 tiles in 8-wave
+    // workgroups, alternating on one box; level over 1000 turns (126.0k against 125.8k) and in
+    // tile sweeps (34.0 us per turn; profiles/r06_headline_pin_ab.log; K = 24 on 30 x 528 12-wave
+    // tiles: 112k)
+    {65536, 65536, {20, 536, 30, 524, 0}, 34.0f},
     // configs[2]: ORD 1, SEG 12 (west carry), 8-wave workgroups, 14 x 320 tiles; 2.84-2.92 us
     // per turn against 3.06-3.20 for round 4's ORD 1 SEG 6 16-wave pick on the same boxes
     // (profiles/r05_c3_codes_ab.log, two boxes; a third had them level, r05_retune_16384.log)
