@@ -979,17 +979,22 @@ struct KnownShape {
     float us_per_turn;                       // measured steady state (round-4 sweeps)
 };
 constexpr KnownShape kKnownShapes[] = {
-    // configs[3..4]: ORD 5, SEG 24 (6 waves per SIMD), K = 20 on 30 x 536 tiles in 12-wave
-    // workgroups (2 per CU): the driver's 20-turn call is one launch of exactly this depth,
-    // 117.8-120.1k GCUPS against 115.9-118.4k for round 5's K = 24 on 30 x 336 tiles in 8-wave
-    // workgroups, alternating on one box; level over 1000 turns (126.0k against 125.8k) and in
-    // tile sweeps (34.0 us per turn; profiles/r06_headline_pin_ab.log; K = 24 on 30 x 528 12-wave
-    // tiles: 112k)
-    {65536, 65536, {20, 536, 30, 524, 0}, 34.0f},
-    // configs[2]: ORD 1, SEG 12 (west carry), 8-wave workgroups, 14 x 320 tiles; 2.84-2.92 us
-    // per turn against 3.06-3.20 for round 4's ORD 1 SEG 6 16-wave pick on the same boxes
-    // (profiles/r05_c3_codes_ab.log, two boxes; a third had them level, r05_retune_16384.log)
-    {16384, 16384, {32, 320, 14, 112, 0}, 2.88f},
+#ifdef GOL_PIN_OVERRIDE   // (A/B builds: an entry ahead of the table, e.g. 65536,65536,{20,472,30,516,0},34.f)
+    {GOL_PIN_OVERRIDE},
+#endif
+    // configs[3..4]: K = 20 (the driver's 20-turn call is one launch of exactly this depth) on
+    // 30 x 472 tiles of ORD 5 SEG 16 in 16-wave workgroups (2 per CU, 8 waves per SIMD): the
+    // fastest of 30 K = 20 shapes (33.6 us per turn; profiles/r06_headline_pin_ab.log) and, in
+    // the bench, 118.3-121.0k against 117.7-119.4k for 30 x 536 SEG 24 12-wave tiles and
+    // 115.9-118.4k for round 5's K = 24 on 30 x 336 8-wave tiles (alternating on one box; 1000
+    // turns 126.8k against 125.8k; K = 24 on 30 x 528 12-wave tiles: 112k)
+    {65536, 65536, {20, 472, 30, 516, 0}, 33.6f},
+    // configs[2]: ORD 5, SEG 16, 8-wave workgroups, 14 x 448 tiles: 2.85 us per turn, the
+    // fastest of 36 K = 32 shapes, and in the bench 94.8-95.0k against 94.0-94.2k for round 5's
+    // 14 x 320 ORD 1 SEG 12 (alternating, profiles/r06_headline_pin_ab.log; that one had beaten
+    // round 4's ORD 1 SEG 6 16-wave pick, 2.84-2.92 against 3.06-3.20 us per turn,
+    // profiles/r05_c3_codes_ab.log)
+    {16384, 16384, {32, 448, 14, 516, 0}, 2.85f},
     // configs[1]: ORD 2, SEG 3, 16-wave workgroups; 0.57-0.59 us per turn (BENCH_r04)
     {5120, 5120, {32, 128, 14, 203, 0}, 0.58f},
     // configs[3..4] as row strips with 128-row halos (buffer = H / N + 256 rows):

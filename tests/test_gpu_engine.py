@@ -523,13 +523,13 @@ def test_driver_command_digest(gol, monkeypatch, pin):
     """The driver's bench command at the headline size (bench.py --steps 20 --warmup 5):
     65536^2 seed 3, one gol_step of 5 turns, then one of 20, against the oracle digest of 25
     turns -- with the engine's own choice (the pinned MI355X shape: one k_step_tile launch of
-    20 turns on 30 x 536 tiles of ORD 5 SEG 24, code 524, 12-wave workgroups, the launch the
+    20 turns on 30 x 472 tiles of ORD 5 SEG 16, code 516, 16-wave workgroups, the launch the
     driver's bench line times), with
     that launch forced through GOL_TILE, and with the create-time search (GOL_AUTOTUNE=2)."""
     if pin == "tile":
         monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
-        monkeypatch.setenv("GOL_TILE", "30,524")
-        kw = dict(band_rows=536, turns_per_launch=20)
+        monkeypatch.setenv("GOL_TILE", "30,516")
+        kw = dict(band_rows=472, turns_per_launch=20)
     elif pin == "search":
         monkeypatch.setenv("GOL_AUTOTUNE", "2")
         kw = {}
@@ -541,8 +541,8 @@ def test_driver_command_digest(gol, monkeypatch, pin):
         e.step(5)
         e.step(20)
         if pin != "search":
-            assert [(k, v, b) for k, v, b in e.last_launches()] == [(20, 15, 536)]
-            assert [(t[0], t[1]) for t in e.last_launch_tiles(blocks=True)] == [(30, 524)]
+            assert [(k, v, b) for k, v, b in e.last_launches()] == [(20, 15, 472)]
+            assert [(t[0], t[1]) for t in e.last_launch_tiles(blocks=True)] == [(30, 516)]
         assert e.info().shape_source == {None: 2, "tile": 0, "search": 1}[pin]
         assert e.snapshot() == (25, d["alive"])
         assert hashlib.sha256(e.read_packed().tobytes()).hexdigest() == d["sha256"]
@@ -575,7 +575,7 @@ def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key, code):
 # the pinned MI355X launch shapes (gol_engine.cpp kKnownShapes): board -> (K, tile height, tile
 # width in lanes, segment code); the bench's configs run exactly these, and profiles/ has a
 # kernel-trace + PMC summary of each
-PINNED_SHAPES = {65536: (20, 536, 30, 524), 16384: (32, 320, 14, 112), 5120: (32, 128, 14, 203)}
+PINNED_SHAPES = {65536: (20, 472, 30, 516), 16384: (32, 448, 14, 516), 5120: (32, 128, 14, 203)}
 # ... and for row strips, by (board width, buffer rows = owned rows + 2 x halo): 65536^2 as N
 # strips with 128-row halos and with the bench's 20-row halos for its 20-turn command, and
 # 16384^2 as 2 strips with 128-row halos (configs[2] on 2 GPUs)
@@ -593,8 +593,8 @@ def test_pinned_shape_digest(gol, key):
     """Each BASELINE board size runs its pinned shape (no create-time search: the kernel the
     bench times is the one profiles/ measured, on every box) and matches the oracle's
     full-size digest -- the shapes of PINNED_SHAPES: 65536^2 x 1000 (configs[3], K = 20 on
-    30 x 536 tiles of ORD 5 SEG 24 in 12-wave workgroups: 50 x 20 turns), 16384^2 x 10000
-    (configs[2], K = 32 on 14 x 320 tiles of ORD 1 SEG 12), 5120^2 x 1000 (configs[1], K = 32
+    30 x 472 tiles of ORD 5 SEG 16 in 16-wave workgroups: 50 x 20 turns), 16384^2 x 10000
+    (configs[2], K = 32 on 14 x 448 tiles of ORD 5 SEG 16), 5120^2 x 1000 (configs[1], K = 32
     on 14 x 128 tiles of ORD 2 SEG 3)."""
     d = _digests()[key]
     K, th, tw, code = PINNED_SHAPES[d["width"]]
