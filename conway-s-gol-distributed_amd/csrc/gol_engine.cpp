@@ -1008,12 +1008,13 @@ constexpr KnownShape kKnownShapes[] = {
     {65536, 33024, {32, 704, 14, 524, 0}, 18.4f},
     // configs[3..4] as row strips with the bench's default halo for its 20-turn command
     // (min(128, turns): 20 rows, one exchange and one 20-turn launch per window; buffer = H / N
-    // + 40 rows): ORD 1 SEG 12 (west carry) on 14 x 344 tiles, K = 20, the fastest of 30-44
-    // shapes at every N (N = 8 / 4 / 2: 4.95 / 9.28 / 18.16 us per turn; ORD 5 SEG 12 5.11 /
-    // -, ORD 5 SEG 24 5.29 / 9.44 / 18.29; profiles/r06_strip_sweep.log)
+    // + 40 rows), K = 20, the fastest of 40-50 shapes swept per buffer
+    // (profiles/r06_strip_sweep.log): N = 8 ORD 1 SEG 12 (west carry) on 14 x 344 tiles, 4.95
+    // us per turn; N = 4 and 2 the headline's ORD 5 SEG 16 on 30 x 472 tiles in 16-wave
+    // workgroups, 9.04 / 17.56 against 9.28-9.36 / 18.16 for 14 x 344 ORD 1 SEG 12
     {65536, 8232, {20, 344, 14, 112, 0}, 4.95f},
-    {65536, 16424, {20, 344, 14, 112, 0}, 9.28f},
-    {65536, 32808, {20, 344, 14, 112, 0}, 18.16f},
+    {65536, 16424, {20, 472, 30, 516, 0}, 9.04f},
+    {65536, 32808, {20, 472, 30, 516, 0}, 17.56f},
     // configs[2] on 2 GPUs: 16384^2 as 2 strips with 128-row halos (16384 x 8448): ORD 5 SEG 12
     // on 30 x 320 tiles, K = 32, 16-wave workgroups: 1.72 us per turn (30 x 320 ORD 1 SEG 12
     // 1.73, 14 x 704 ORD 5 SEG 12 1.74, the 14 x 320 ORD 1 torus pin slower;

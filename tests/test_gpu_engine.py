@@ -582,8 +582,8 @@ PINNED_SHAPES = {65536: (20, 472, 30, 516), 16384: (32, 448, 14, 516), 5120: (32
 PINNED_STRIP_SHAPES = {
     (65536, 8448): (16, 352, 14, 112), (65536, 16640): (32, 704, 14, 524),
     (65536, 33024): (32, 704, 14, 524),
-    (65536, 8232): (20, 344, 14, 112), (65536, 16424): (20, 344, 14, 112),
-    (65536, 32808): (20, 344, 14, 112),
+    (65536, 8232): (20, 344, 14, 112), (65536, 16424): (20, 472, 30, 516),
+    (65536, 32808): (20, 472, 30, 516),
     (16384, 8448): (32, 320, 30, 512)}
 
 
