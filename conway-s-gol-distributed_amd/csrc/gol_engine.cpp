@@ -1001,11 +1001,12 @@ constexpr KnownShape kKnownShapes[] = {
     // N = 8 ORD 1 SEG 12 (west carry) on 14 x 352 tiles, 8 launches of 16 turns per window
     // (5.44-5.46 us per turn against 5.69-5.70 for ORD 5 SEG 12 on the same tiles,
     // profiles/r05_strip_seg12_ab.log; 5.61-5.71 for round 4's searched picks); N = 4 and 2
-    // ORD 5 SEG 24 on 14 x 704 tiles (tile sweeps over the strip shapes,
-    // profiles/r05_strip_sweep.log)
+    // ORD 5 SEG 16 since round 6: 14 x 448 tiles K = 32 (9.14 against 9.21 us per turn for
+    // round 5's 14 x 704 SEG 24) and 14 x 480 tiles K = 16 (16.97 against 17.91)
+    // (profiles/r06_strip_sweep.log)
     {65536, 8448, {16, 352, 14, 112, 0}, 5.3f},
-    {65536, 16640, {32, 704, 14, 524, 0}, 9.5f},
-    {65536, 33024, {32, 704, 14, 524, 0}, 18.4f},
+    {65536, 16640, {32, 448, 14, 516, 0}, 9.14f},
+    {65536, 33024, {16, 480, 14, 516, 0}, 16.97f},
     // configs[3..4] as row strips with the bench's default halo for its 20-turn command
     // (min(128, turns): 20 rows, one exchange and one 20-turn launch per window; buffer = H / N
     // + 40 rows), K = 20, the fastest of 40-50 shapes swept per buffer

@@ -580,8 +580,8 @@ PINNED_SHAPES = {65536: (20, 472, 30, 516), 16384: (32, 448, 14, 516), 5120: (32
 # strips with 128-row halos and with the bench's 20-row halos for its 20-turn command, and
 # 16384^2 as 2 strips with 128-row halos (configs[2] on 2 GPUs)
 PINNED_STRIP_SHAPES = {
-    (65536, 8448): (16, 352, 14, 112), (65536, 16640): (32, 704, 14, 524),
-    (65536, 33024): (32, 704, 14, 524),
+    (65536, 8448): (16, 352, 14, 112), (65536, 16640): (32, 448, 14, 516),
+    (65536, 33024): (16, 480, 14, 516),
     (65536, 8232): (20, 344, 14, 112), (65536, 16424): (20, 472, 30, 516),
     (65536, 32808): (20, 472, 30, 516),
     (16384, 8448): (32, 320, 30, 512)}
