@@ -75,6 +75,11 @@ __device__ __forceinline__ void tile_turn_asm(uint32_t (&v)[SEG][2], uint32_t (&
 #ifndef GOL_TILE_RAW
 #define GOL_TILE_RAW 0
 #endif
+// ORD 3 = two tiles per workgroup, software-pipelined (tile_pass_pair; A/B builds: make variant
+// VDEFS=-DGOL_TILE_PAIR=1).  Without it ORD 3 is the tools build's no-barrier timing ablation.
+#ifndef GOL_TILE_PAIR
+#define GOL_TILE_PAIR 0
+#endif
 template <int SEG, int W>
 constexpr bool tile_west_carry() { return GOL_TILE_WEST_CARRY && W == 1 && SEG >= 4 && SEG <= 16; }
 
@@ -112,7 +117,8 @@ constexpr size_t tile_lds_bytes_code(int threads, int code)
     const int ord = code / 100 % 10;
     return (ord == 8 || ord == 9) && (GOL_TURN_VAR & 4)
                ? tile_lds_bytes(tile_slots_pow2(threads), 1)
-               : tile_lds_bytes(threads, tile_seg_words(code));
+           : ord == 3 && GOL_TILE_PAIR ? 2 * tile_lds_bytes(threads, 1)   // (two tiles' slots)
+                                       : tile_lds_bytes(threads, tile_seg_words(code));
 }
 
 // W words per lane (2W dwords, interleaved layout word by word).  With W = 2 the lane's two
@@ -631,6 +637,209 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     }
 }
 
+// ORD 3 (round 6): two tiles per workgroup, software-pipelined (the round-5 verdict's ask for
+// small boards, whose turn is a serial chain: one barrier, the LDS round trip of the edge sums,
+// the edge rules, the next turn's row sums and stores, then the barrier again -- the waves of a
+// workgroup all reach each phase together, so the VALU idles while the LDS works and back).
+// Every lane holds one SEG-row segment of tile A and one of tile B (the same local rows of two
+// tiles), and each turn is split in two halves:
+//   H1(X) -- the row sums of the segment's first and last rows, their stores to LDS, and the
+//            interior rows (everything that needs no neighbour);
+//   H2(X) -- the neighbours' edge sums read back and the first and last rows' rules.
+// Between two workgroup barriers a lane runs H2 of one tile beside H1 of the other, so one
+// tile's LDS reads are in flight while the other tile's VALU work issues:
+//   H1(A, 0) | H2(A, t), H1(B, t) | H2(B, t), H1(A, t + 1) | ...
+// Two barriers per turn for two tiles: one per tile-turn, as for one tile.  The edge sums stay
+// double-buffered by turn parity per tile ([tile][parity][top, bottom][slot]).  One word per
+// lane; segments of 2..8 rows.
+template <int SEG>
+__device__ __forceinline__ void tile_pass_pair(const uint64_t *__restrict__ in,
+                                               uint64_t *__restrict__ out, const StepArgs &a,
+                                               int turns, int tileA, int tileB, bool storeB,
+                                               int ntx)
+{
+    constexpr int ND = 2, NS = 4;
+    static_assert(SEG >= 2 && SEG <= 8, "ORD 3: short segments");
+    extern __shared__ uint4 xsh[];
+    const int nslot = (int)blockDim.x;
+    const int TW = a.tile_w, C = TW + 2, G = 64 / C;
+    const int K = turns, TH = a.band;
+    const int nl = a.nw;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int group = lane / C, col = lane - group * C;
+    const bool live = group < G;
+    const int nseg = (TH + 2 * K + SEG - 1) / SEG;
+    const int seg = wave * G + group;
+    const int slot = seg * C + col;
+    const int M = a.modrows;
+    const uint32_t pitch_b = (uint32_t)a.pitch * 8u;
+    const uint32_t span = (uint32_t)M * pitch_b;
+    const __amdgpu_buffer_rsrc_t rin =
+        __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)span, kBufFlags);
+    const __amdgpu_buffer_rsrc_t rout =
+        __builtin_amdgcn_make_buffer_rsrc((void *)out, (short)0, (int)span, kBufFlags);
+    const int tiles[2] = {tileA, tileB};
+    uint32_t v[2][SEG][ND];
+    int y0s[2], x0s[2];
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+        const int ty = tiles[X] / ntx, tx = tiles[X] - ty * ntx;
+        y0s[X] = a.row_lo + ty * TH;
+        x0s[X] = tx * TW;
+        int gx = x0s[X] - 1 + (live ? col : 0);
+        while (gx < 0) gx += nl;
+        while (gx >= nl) gx -= nl;
+        int r = y0s[X] - K + (live ? seg : 0) * SEG;
+        while (r < 0) r += M;
+        while (r >= M) r -= M;
+        uint32_t off = (uint32_t)r * pitch_b + (uint32_t)gx * 8u;
+#pragma unroll
+        for (int i = 0; i < SEG; ++i) {
+            const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, 0);
+            v[X][i][0] = w.x;
+            v[X][i][1] = w.y;
+            off += pitch_b;
+            off = off >= span ? off - span : off;
+        }
+    }
+    auto rsum = [&](const uint32_t (&x)[ND], uint32_t (&s)[NS]) {
+        const uint32_t Rt = dpp_from_upper_z(x[0]);
+        const uint32_t e = x[0], o = x[1];
+        uint32_t wl;
+        if constexpr (tile_west_carry<SEG, 1>()) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64((int)o < 0) << 1;
+            uint64_t co;
+            asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(wl), "=&s"(co) : "v"(o), "s"(m));
+        } else {
+            wl = __builtin_amdgcn_alignbit(o, dpp_from_lower_z(o), 31);
+        }
+        const uint32_t er = __builtin_amdgcn_alignbit(Rt, e, 1);
+        s[0] = xor3(wl, e, o);
+        s[1] = maj(wl, e, o);
+        s[2] = xor3(e, o, er);
+        s[3] = maj(e, o, er);
+    };
+    auto rule = [&](const uint32_t (&A)[NS], const uint32_t (&B)[NS], const uint32_t (&Cs)[NS],
+                    uint32_t (&x)[ND]) {
+        uint32_t n[ND];
+#pragma unroll
+        for (int d = 0; d < ND; ++d)
+            n[d] = life_rule7(A[2 * d], B[2 * d], Cs[2 * d], A[2 * d + 1], B[2 * d + 1],
+                              Cs[2 * d + 1], x[d]);
+#pragma unroll
+        for (int d = 0; d < ND; ++d) x[d] = n[d];
+    };
+    auto put = [&](uint4 *p, const uint32_t (&S)[NS]) { *p = make_uint4(S[0], S[1], S[2], S[3]); };
+    auto get = [&](const uint4 *p, uint32_t (&S)[NS]) {
+        const uint4 u = *p;
+        S[0] = u.x;
+        S[1] = u.y;
+        S[2] = u.z;
+        S[3] = u.w;
+    };
+    // slots as in tile_pass: idle lanes own the slots past the tile's, a segment with no
+    // neighbour reads its own (junk that reaches only the tile's outermost row)
+    const int nlive = (int)(blockDim.x >> 6) * G * C;
+    const int myslot = live ? slot : nlive + wave * (64 - G * C) + (lane - G * C);
+    const int s_up = live && seg > 0 ? slot - C : myslot;
+    const int s_dn = live && seg + 1 < nseg ? slot + C : myslot;
+    // [tile X][parity p][top 0 / bottom 1][slot]
+    auto at = [&](int X, int p, int bt, int sl) { return xsh + ((X * 2 + p) * 2 + bt) * nslot + sl; };
+    uint32_t F[2][NS], Lr[2][NS], S1[2][NS], Pl[2][NS];
+    auto h1 = [&](auto XX, auto PP) {
+        constexpr int X = decltype(XX)::value, p = decltype(PP)::value;
+        rsum(v[X][0], F[X]);
+        rsum(v[X][SEG - 1], Lr[X]);
+        put(at(X, p, 0, myslot), F[X]);
+        put(at(X, p, 1, myslot), Lr[X]);
+        uint32_t Pw[NS], Q[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) Pw[k] = F[X][k];
+        if constexpr (SEG >= 3) {
+            rsum(v[X][1], Q);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NS; ++k) Q[k] = Lr[X][k];
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k) S1[X][k] = Q[k];
+#pragma unroll
+        for (int i = 1; i + 1 < SEG; ++i) {
+            uint32_t R[NS];
+            if (i + 2 == SEG) {
+#pragma unroll
+                for (int k = 0; k < NS; ++k) R[k] = Lr[X][k];
+            } else {
+                rsum(v[X][i + 1], R);
+            }
+            rule(Pw, Q, R, v[X][i]);
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
+                Pw[k] = Q[k];
+                Q[k] = R[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k) Pl[X][k] = Pw[k];   // sums of row SEG-2 (row 0 at SEG 2)
+    };
+    auto h2 = [&](auto XX, auto PP) {
+        constexpr int X = decltype(XX)::value, p = decltype(PP)::value;
+        uint32_t U[NS], D[NS];
+        get(at(X, p, 1, s_up), U);
+        get(at(X, p, 0, s_dn), D);
+        rule(U, F[X], S1[X], v[X][0]);
+        rule(Pl[X], Lr[X], D, v[X][SEG - 1]);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    const int lastrow = 2 * K + TH - 1;
+    const int wrow0 = wave * G * SEG, wrow1 = wrow0 + G * SEG;
+    auto leaves = [&](int t) { return wrow1 <= t || wrow0 > lastrow - t; };   // (wave-uniform)
+    h1(I0{}, I0{});
+    __syncthreads();
+    bool gone = false;
+    for (int t = 0; t < K; t += 2) {
+        if (leaves(t)) {
+            gone = true;
+            break;
+        }
+        h2(I0{}, I0{});
+        h1(I1{}, I0{});
+        __syncthreads();
+        h2(I1{}, I0{});
+        if (t + 1 == K) break;
+        h1(I0{}, I1{});
+        __syncthreads();
+        if (leaves(t + 1)) {
+            gone = true;
+            break;
+        }
+        h2(I0{}, I1{});
+        h1(I1{}, I1{});
+        __syncthreads();
+        h2(I1{}, I1{});
+        if (t + 2 == K) break;
+        h1(I0{}, I0{});
+        __syncthreads();
+    }
+    if (gone || !live || col < 1 || col > TW) return;
+    // interior rows [K, K + TH) of each tile below row_hi, interior columns inside the row
+    const int t0 = seg * SEG;
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+        if (X == 1 && !storeB) break;
+        if (x0s[X] + col - 1 >= nl) continue;
+        uint32_t so = (uint32_t)(y0s[X] - K + t0) * pitch_b + (uint32_t)(x0s[X] + col - 1) * 8u;
+#pragma unroll
+        for (int i = 0; i < SEG; ++i) {
+            const int tr = t0 + i;
+            if (tr >= K && tr < K + TH && y0s[X] - K + tr < a.row_hi) buf_store(v[X][i], rout, so, 0);
+            so += pitch_b;
+        }
+    }
+}
+
 // XCD-aware tile order: blockIdx b runs on XCD b % 8, which gets a contiguous run of tiles
 // (whole tile rows, so most halo rows were written by the same XCD's L2)
 __device__ __forceinline__ int tile_of_block(int ntiles)
@@ -648,6 +857,20 @@ __global__ __launch_bounds__(1024, (ORD == 7 ? 6 : 1)) void k_step_tile(const ui
     const int tile = tile_of_block(ntiles);
     if (tile >= ntiles) return;                          // the whole workgroup
     tile_pass<SEG, ORD, W, false>(in, out, a, turns, tile, ntx);
+}
+
+// ORD 3: tile pairs (tile_pass_pair).  Pair j runs tiles 2j and 2j + 1; with an odd count the
+// last pair repeats its first tile and stores it once.
+template <int SEG>
+__global__ __launch_bounds__(1024, 1) void k_step_tile_pair(const uint64_t *__restrict__ in,
+                                                            uint64_t *__restrict__ out, StepArgs a,
+                                                            int turns, int ntx, int ntiles)
+{
+    const int npairs = (ntiles + 1) / 2;
+    const int pair = tile_of_block(npairs);
+    if (pair >= npairs) return;                          // the whole workgroup
+    const int tA = 2 * pair, tB = 2 * pair + 1 < ntiles ? 2 * pair + 1 : 2 * pair;
+    tile_pass_pair<SEG>(in, out, a, turns, tA, tB, 2 * pair + 1 < ntiles, ntx);
 }
 
 // K1p k_tile_persist: `turns` turns in blocks of K on tiles that stay resident for the whole

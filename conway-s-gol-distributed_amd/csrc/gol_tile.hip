@@ -119,7 +119,18 @@ void *tile_kernel(int code)
     if (code == 1112) return reinterpret_cast<void *>(&k_step_tile<12, 1, 2>);
     if (code == 1512) return reinterpret_cast<void *>(&k_step_tile<12, 5, 2>);
 #endif
-#if GOL_TOOLS   // ORD 3: no barrier between turns (wrong boards): what the turn's sync costs
+#if GOL_TILE_PAIR   // ORD 3: two tiles per workgroup, software-pipelined (tile_pass_pair)
+    if (ord == 3 && w == 1) {
+        switch (seg) {
+        case 2: return reinterpret_cast<void *>(&k_step_tile_pair<2>);
+        case 3: return reinterpret_cast<void *>(&k_step_tile_pair<3>);
+        case 4: return reinterpret_cast<void *>(&k_step_tile_pair<4>);
+        case 6: return reinterpret_cast<void *>(&k_step_tile_pair<6>);
+        case 8: return reinterpret_cast<void *>(&k_step_tile_pair<8>);
+        default: return nullptr;
+        }
+    }
+#elif GOL_TOOLS   // ORD 3: no barrier between turns (wrong boards): what the turn's sync costs
     if (ord == 3 && w == 1) return tile_fn<3, 1>(seg);
 #endif
     if (code < 0 || w > 2) return nullptr;
@@ -155,7 +166,7 @@ bool tile_shape_ok(int nw, int turns, int tile_h, int tile_w, int seg)
     if (turns < 2 || turns > 64 || tile_h < 1 || tile_w < 1 || tile_w + 2 > 64 || !tile_kernel(seg))
         return false;
     if (!GOL_TOOLS && !tile_code_shipped(seg) && !(GOL_TILE_W2_SEG12 && seg % 1000 == 112) &&
-        !(GOL_TILE_W2_SEG12 && seg % 1000 == 512))
+        !(GOL_TILE_W2_SEG12 && seg % 1000 == 512) && !(GOL_TILE_PAIR && seg / 100 == 3))
         return false;   // (untested instantiations)
     if (nw % tile_seg_words(seg)) return false;          // (whole word pairs per lane)
     const int C = tile_w + 2, G = 64 / C;
@@ -210,7 +221,9 @@ hipError_t launch_tile(const StepArgs &a, int turns, hipStream_t s)
     const int ntx = (a.nw / tile_seg_words(a.tile_seg) + a.tile_w - 1) / a.tile_w;
     const long long ntiles = (long long)ntx * ((rows + a.band - 1) / a.band);
     if (ntiles <= 0 || ntiles > (1 << 24)) return hipErrorInvalidValue;
-    const unsigned blocks = (unsigned)((ntiles + 7) / 8 * 8);
+    // (ORD 3 with GOL_TILE_PAIR: one workgroup per pair of tiles)
+    const long long units = GOL_TILE_PAIR && a.tile_seg / 100 == 3 ? (ntiles + 1) / 2 : ntiles;
+    const unsigned blocks = (unsigned)((units + 7) / 8 * 8);
     const int threads = 64 * tile_waves(turns, a.band, a.tile_w, a.tile_seg);
     void *fn = tile_kernel(a.tile_seg);
     StepArgs args = a;
