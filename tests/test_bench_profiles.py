@@ -77,3 +77,43 @@ def test_pinned_shapes_have_profiles():
         # (against every buffer row: the passes ran a torus of the strip's buffer height)
         cpi, infl = b.valu_figures(d, size * shape["buffer_rows"], shape["turns"])
         assert infl and 1.0 < infl < 2.0, (src, infl)
+
+
+def test_valu_figures_from_summary():
+    """bench.valu_figures on the committed headline summary: SIMD cycles per VALU = dispatch time
+    x measured clock / (SQ_INSTS_VALU / 1024), and VALU inflation = SQ_INSTS_VALU / the useful 22
+    VALU per 4096 cell-updates; the issue-model roof is 193.6k GCUPS and never below anything
+    the kernel reaches (verdict r05 weak #2)."""
+    b = _bench()
+    d = json.load(open(os.path.join(ROOT, "profiles", "r06_k20_65536_h_summary.json")))
+    cpi, infl = b.valu_figures(d, 65536 * 65536, 20)
+    sq = d["sq_counters_median"]
+    want_cpi = d["sq_dispatch_us_median"] * 1e3 * d["clock_ghz"] / (sq["SQ_INSTS_VALU"] / 1024)
+    assert abs(cpi - want_cpi) < 1e-3 and 2.36 <= cpi < 4.0       # (52 / 22 = 2.36: the model)
+    assert abs(infl - sq["SQ_INSTS_VALU"] / (65536 * 65536 * 20 / 4096 * 22)) < 1e-4
+    assert 1.0 < infl < 1.3
+    assert abs(b.VALU_PEAK_GCUPS - 1024 * 2.4e9 / 52 * 4096 / 1e9) < 1e-6
+    # the headline's own rate at the measured clock stays under the roof at that clock
+    line = d["bench_line"]
+    assert line["value"] < b.VALU_PEAK_GCUPS * d["clock_ghz"] / 2.4
+    assert b.valu_figures(None, 1, 1) == (None, None)
+
+
+def test_exchange_fields_and_launch_shape():
+    """The N > 1 fields of a bench line (bench.exchange_fields) and the launch shape's buffer
+    rows (bench.launch_shape): a strip's shape never matches a torus summary of the same tile."""
+    b = _bench()
+    c = {"exchanges": 1, "halo": 20, "exchange_us": [[12.5, 1, 12.5], [14.0, 1, 14.0]],
+         "compute_only": {"steps": 20, "wall": 1e-4, "exchanges": 0}, "W": 65536, "H": 65536}
+    f = b.exchange_fields(c)
+    assert f["exchanges_timed"] == 1 and f["halo"] == 20
+    assert [x["rank"] for x in f["exchange_us_per_rank"]] == [0, 1]
+    assert f["exchange_us_per_rank"][1]["mean_us"] == 14.0
+    assert f["compute_only"]["exchanges_timed"] == 0
+    assert abs(f["compute_only"]["value"] - 65536 * 65536 * 20 / 1e-4 / 1e9) < 1e-3
+    plan, tiles = [(20, 15, 344)], [(14, 112, 8, 20)]
+    sh = b.launch_shape(plan, tiles, 15, 20, 8232)
+    assert sh["buffer_rows"] == 8232 and sh["tile"]["code"] == 112
+    assert sh["tile"]["waves_per_workgroup"] == 8
+    d, src = b.pmc_summary(65536, 20, sh)
+    assert src == os.path.join("profiles", "r06_k20_65536_s8_summary.json"), src
