@@ -243,13 +243,13 @@ class RcclComm:
                                   self.comm, s), "ncclRecv")
         finally:
             rc = L.ncclGroupEnd()
-        if rc == NCCL_IN_PROGRESS:
+        if rc not in (0, NCCL_IN_PROGRESS):
+            _check(rc, "ncclGroupEnd")
+        if rc == NCCL_IN_PROGRESS or self._state() != 0:
             # (non-blocking communicator: the first group also connects the peers; the ops are
             # on the stream once the state is ncclSuccess, so the caller's next launch on the
-            # same stream is ordered after them)
+            # same stream -- and the next RCCL call -- come after them)
             self._wait("ncclGroupEnd", time.monotonic())
-        else:
-            _check(rc, "ncclGroupEnd")
 
     def close(self):
         if self.comm:
