@@ -195,24 +195,52 @@ class DistStrip:
         self._stale = False
         stream = getattr(self.strip, "stream", None)
         pair = self._ev_begin(stream) if stream is not None else None
-        ctx = getattr(self.strip, "stream_context", None)
-        if ctx is None:
-            self._exchange()
+        if self.rccl is not None and getattr(self.strip, "zero_copy", False):
+            self._exchange_rccl_direct()
         else:
-            with ctx():
+            ctx = getattr(self.strip, "stream_context", None)
+            if ctx is None:
                 self._exchange()
+            else:
+                with ctx():
+                    self._exchange()
         if stream is not None:
             self._ev_end(pair, stream)
+
+    def _exchange_rccl_direct(self):
+        """The bench's exchange (direct RCCL, zero-copy board rows): four device pointers from
+        gol_halo_buffers straight into one RCCL group on the engine's stream, then
+        gol_halo_done -- no torch tensor views and no stream context, because a timed window
+        starts with this call on an idle GPU and every microsecond of host work before the
+        first enqueue is in the window (tools/xchg_overhead.py: ~29 us through the tensor path
+        at the 8-strip shape)."""
+        eng = self.strip.engine
+        (st, sb, rt, rb), lay = eng.halo_buffers()
+        self.strip.layout = lay
+        if not self._layout_checked:
+            self._check_layout_value(lay, self.strip.device)
+        self.rccl.exchange(((st, self.up), (sb, self.down)), ((rb, self.down), (rt, self.up)),
+                           self._nbytes(eng), self.strip.stream.cuda_stream)
+        eng.halo_done()
+        self.exchanges += 1
+
+    def _nbytes(self, eng):
+        n = getattr(self, "_msg_bytes", None)
+        if n is None:
+            n = self._msg_bytes = int(eng.halo) * int(eng.words_per_row) * 8
+        return n
 
     def _check_layout(self, like):
         """Zero-copy messages carry the engines' stepping layout: every rank must agree
         (equal width, halo and flags guarantee it; checked once, before the first
         exchange, with one tiny all-reduce)."""
+        self._check_layout_value(getattr(self.strip, "layout", None), like.device)
+
+    def _check_layout_value(self, lay, device):
         self._layout_checked = True
-        lay = getattr(self.strip, "layout", None)
         if lay is None:
             return
-        dev = like.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        dev = device if dist.get_backend(self.group) == "nccl" else "cpu"
         t = torch.tensor([lay], dtype=torch.int64, device=dev)
         dist.all_reduce(t, group=self.group)
         if int(t.item()) not in (0, self.world):
@@ -273,17 +301,25 @@ class DistStrip:
 
     def step(self, turns: int):
         turns = int(turns)
+        hv = None                               # turns the halos have left (queried once)
         while turns > 0:
-            if self.strip.halo_valid == 0 or self._stale:
+            if hv is None:
+                hv = self.strip.halo_valid
+            if hv == 0 or self._stale:
                 if self.overlap:
                     n = min(turns, self.strip.engine.halo)
                     self._exchange_overlapped(n)
                     turns -= n
+                    hv = None
                     continue
                 self.exchange()
-            n = min(turns, self.strip.halo_valid)
+                # (fresh halos: an engine strip's depth, without another query)
+                eng = getattr(self.strip, "engine", None)
+                hv = int(eng.halo) if eng is not None else self.strip.halo_valid
+            n = min(turns, hv)
             self.strip.step(n)
             turns -= n
+            hv -= n
 
 
 def make_engine_strip(width: int, height: int, rank: int, world: int, halo: int,

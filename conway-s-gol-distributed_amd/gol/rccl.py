@@ -234,13 +234,18 @@ class RcclComm:
         matching between a pair of ranks holds even when both neighbours are one rank."""
         L = lib()
         s = ctypes.c_void_p(int(stream_ptr))
-        _check(L.ncclGroupStart(), "ncclGroupStart")
+        comm, send, recv = self.comm, L.ncclSend, L.ncclRecv
+        rc = L.ncclGroupStart()
+        if rc != 0:
+            _check(rc, "ncclGroupStart")
         try:
             for (sp, speer), (rp, rpeer) in zip(sends, recvs):
-                _check(L.ncclSend(ctypes.c_void_p(sp), nbytes, NCCL_INT8, int(speer),
-                                  self.comm, s), "ncclSend")
-                _check(L.ncclRecv(ctypes.c_void_p(rp), nbytes, NCCL_INT8, int(rpeer),
-                                  self.comm, s), "ncclRecv")
+                rc = send(sp, nbytes, NCCL_INT8, speer, comm, s)
+                if rc != 0:
+                    _check(rc, "ncclSend")
+                rc = recv(rp, nbytes, NCCL_INT8, rpeer, comm, s)
+                if rc != 0:
+                    _check(rc, "ncclRecv")
         finally:
             rc = L.ncclGroupEnd()
         if rc not in (0, NCCL_IN_PROGRESS):
