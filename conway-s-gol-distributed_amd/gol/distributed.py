@@ -147,13 +147,18 @@ class DistStrip:
         self._stale = False            # start_window(): the next step exchanges first
         self._ev_pool = []             # time_exchanges(): HIP event pairs not yet used
         self._ev_used = []
+        self._ptrs = None              # start_window(): the board rows' pointers, until a step
 
     def start_window(self):
         """Make the next ``step`` begin with an exchange, whatever turns its halos have left:
         a timed region that starts here holds exactly one exchange per ``halo`` turns (the
         run's cadence), not a partial window left over from the warm-up.  (An exchange is
-        valid at any turn: the neighbours' owned rows are exact.)"""
+        valid at any turn: the neighbours' owned rows are exact.)  On the direct RCCL path the
+        board rows' device pointers are looked up here already (they stay valid until the next
+        step), so the exchange that opens the window only enqueues."""
         self._stale = True
+        if self.rccl is not None and getattr(self.strip, "zero_copy", False) and not self.overlap:
+            self._ptrs = self.strip.engine.halo_buffers()
 
     def time_exchanges(self, n: int):
         """Bracket each of the next ``n`` exchanges with a HIP event pair on the stream the
@@ -215,7 +220,8 @@ class DistStrip:
         first enqueue is in the window (tools/xchg_overhead.py: ~29 us through the tensor path
         at the 8-strip shape)."""
         eng = self.strip.engine
-        (st, sb, rt, rb), lay = eng.halo_buffers()
+        ptrs, self._ptrs = self._ptrs, None
+        (st, sb, rt, rb), lay = ptrs if ptrs is not None else eng.halo_buffers()
         self.strip.layout = lay
         if not self._layout_checked:
             self._check_layout_value(lay, self.strip.device)
@@ -308,6 +314,7 @@ class DistStrip:
             if hv == 0 or self._stale:
                 if self.overlap:
                     n = min(turns, self.strip.engine.halo)
+                    self._ptrs = None
                     self._exchange_overlapped(n)
                     turns -= n
                     hv = None
@@ -317,6 +324,7 @@ class DistStrip:
                 eng = getattr(self.strip, "engine", None)
                 hv = int(eng.halo) if eng is not None else self.strip.halo_valid
             n = min(turns, hv)
+            self._ptrs = None                   # (the board moves: pointers from before are stale)
             self.strip.step(n)
             turns -= n
             hv -= n
