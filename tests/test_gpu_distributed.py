@@ -76,6 +76,20 @@ def test_rccl_self_exchange_65536(overlap):
     assert "world=1 halo=128 exchanges=7" in out and f"overlap={overlap}" in out
 
 
+@pytest.mark.parametrize("halo,tpl,every,digest", [(20, 8, 7, ""), (20, 0, 13, ""),
+                                                   (128, 0, 20, "65536x65536_seed3_t1000")])
+def test_rccl_self_exchange_windows(halo, tpl, every, digest):
+    """The bench's N > 1 timed-region form (round 6): blocks of turns each opened by
+    DistStrip.start_window -- an exchange at any turn, its board pointers looked up before the
+    window (the direct RCCL path) -- over RCCL at world size 1, against the oracle; the last
+    case runs 65536^2 x 1000 in 20-turn windows on 128-row halos against the digest."""
+    args = ["--backend", "nccl", "--transport", "rccl", "--halo", halo, "--tpl", tpl,
+            "--window-every", every]
+    args += ["--digest", digest] if digest else ["--height", 640]
+    out = _dist_check(1, args, 29760 + every + halo)
+    assert "backend=nccl" in out
+
+
 def test_halo_buffers_zero_copy_torus():
     """gol_halo_buffers: the four views are the strip's boundary and halo rows in the
     current board; copying send_bottom -> recv_top and send_top -> recv_bottom on the

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--overlap", action="store_true",
                     help="direct RCCL: exchange on its own stream, overlapped with the first "
                          "launch's interior rows (gol_step_overlap)")
+    ap.add_argument("--window-every", type=int, default=0,
+                    help="step in blocks of this many turns, each opened by DistStrip.start_window "
+                         "(an exchange at any turn, as bench.py's timed region starts)")
     a = ap.parse_args()
     want_digest = None
     if a.digest:
@@ -60,7 +63,15 @@ def main():
         comm = RcclComm(rank, world, dev)
     ds = DistStrip(EngineStrip(eng, dev, zero_copy=not a.copy), rank, world,
                    stage_on_host=a.backend == "gloo", rccl=comm, overlap=a.overlap)
-    ds.step(a.turns)
+    if a.window_every > 0:
+        left = a.turns
+        while left:
+            n = min(left, a.window_every)
+            ds.start_window()
+            ds.step(n)
+            left -= n
+    else:
+        ds.step(a.turns)
     split = gol.strip_split(a.height, world)
     maxr = max(r for _, r in split)
     mine = torch.zeros((maxr, eng.words_per_row), dtype=torch.int64)   # gather: equal sizes
