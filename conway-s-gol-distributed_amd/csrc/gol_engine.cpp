@@ -129,6 +129,7 @@ struct gol_ctx {
     int persist_k = 0;
     int persist_seg = 0;                     // K1p's segment code (plain launches keep tile_seg)
     bool persist_forced = false;             // GOL_PERSIST (tests): also on a shared device
+    bool persist_ring = false;               // GOL_RING (tools build): K1r instead of K1p
     uint64_t *pu[2] = {nullptr, nullptr};
     unsigned *pflags = nullptr;
     size_t pflags_n = 0;
@@ -571,6 +572,8 @@ hipError_t persist_launch(gol_ctx *c, golk::StepArgs a, int turns, int K)
     const unsigned nblocks = (unsigned)((turns + K - 1) / K);
     const unsigned epoch = c->pepoch + 1;
     c->pepoch = epoch + nblocks;
+    if (c->persist_ring)                     // K1r: only the rings pass through u0 / u1
+        return golk::launch_tile_ring(a, turns, K, c->pu[0], c->pu[1], c->pflags, epoch, c->stream);
     return golk::launch_tile_persist(a, turns, K, c->pu[0], c->pu[1], c->pflags, epoch, c->stream);
 }
 
@@ -1878,12 +1881,17 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
         if (const char *v = getenv("GOL_PERSIST")) {       // tests / experiments: K1p blocks
             const int pk = atoi(v);
             if (pk > 0) {
+                const char *rv = getenv("GOL_RING");
+                const bool ring = rv && atoi(rv) > 0;
                 if (c->multi_variant != golk::kMultiTile || is_strip(c) ||
-                    !golk::tile_persist_ok(c->nw, c->buf_rows, 2 * pk, pk, c->band_multi,
-                                           c->tile_w, c->tile_seg, c->ncu))
+                    !(ring ? golk::tile_ring_ok(c->nw, c->buf_rows, pk, c->band_multi, c->tile_w,
+                                                c->tile_seg, c->ncu)
+                           : golk::tile_persist_ok(c->nw, c->buf_rows, 2 * pk, pk, c->band_multi,
+                                                   c->tile_w, c->tile_seg, c->ncu)))
                     return bail(GOL_EINVAL);
                 c->persist_k = pk;
                 c->persist_forced = true;
+                c->persist_ring = ring;
             }
         }
         if (const char *v = getenv("GOL_STREAM")) {        // tests / experiments: K1q blocks

@@ -221,6 +221,8 @@ constexpr int kTilePersistCodes[] = {102, 103, 104, 106, 108, 112, 116,
 // the codes k_tile_stream (K1q) is instantiated for (gol_tile.hip stream_fn; each pinned by
 // tests/test_gpu_engine.py::test_tile_stream_pinned through gol_tile_stream_codes)
 constexpr int kTileStreamCodes[] = {106, 506, 512, 524};
+// the codes k_tile_ring (K1r) is instantiated for in the tools build (gol_tile.hip ring_fn)
+constexpr int kTileRingCodes[] = {103, 203, 503, 504, 506, 508, 512, 516, 112, 116};
 constexpr bool tile_code_shipped(int code)
 {
     for (int c : kTileCodes)
@@ -248,6 +250,11 @@ bool tile_stream_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg);
 hipError_t launch_tile_stream(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
                               unsigned *flags, unsigned epoch, unsigned *counter, unsigned base,
                               int ncu, int max_grid, unsigned *grid, hipStream_t s);
+// K1r k_tile_ring (gol_tile.h): K1p's contract (flags, epoch) with the tiles kept in registers
+// across blocks; only their rings pass through u0 / u1 (uncached, board-sized).
+bool tile_ring_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg, int ncu);
+hipError_t launch_tile_ring(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
+                            unsigned *flags, unsigned epoch, hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);
 

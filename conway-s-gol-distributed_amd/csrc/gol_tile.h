@@ -80,6 +80,11 @@ __device__ __forceinline__ void tile_turn_asm(uint32_t (&v)[SEG][2], uint32_t (&
 #ifndef GOL_TILE_PAIR
 #define GOL_TILE_PAIR 0
 #endif
+// (K1p / K1q / K1r: polls of a neighbour tile's flag before a wait gives up; the test build
+// libgolamd_spin0.so sets 0)
+#ifndef GOL_TILE_SPIN_LIMIT
+#define GOL_TILE_SPIN_LIMIT (1 << 22)
+#endif
 template <int SEG, int W>
 constexpr bool tile_west_carry() { return GOL_TILE_WEST_CARRY && W == 1 && SEG >= 4 && SEG <= 16; }
 
@@ -131,10 +136,19 @@ constexpr size_t tile_lds_bytes_code(int threads, int code)
 // trapezoid computes halo rows nobody reads) and the pass returns on every path.  (A leaving
 // wave would have to meet the barriers of its remaining turns, and that exit path alone took
 // the SEG 24 pass from 80 to 126 VGPRs.)
-template <int SEG, int ORD, int W, bool PERSIST>
+// K1r (RING): the tile stays in registers across blocks; between blocks only its ring is
+// exchanged (k_tile_ring below)
+struct RingArgs {
+    uint64_t *u0, *u1;          // board-layout edge buffers, block b writes u[b % 2]
+    unsigned *flags;            // per tile: epoch + b + 1 once its block-b edges are stored
+    unsigned epoch;
+    int turns;                  // turns of the launch, in blocks of <= K
+};
+template <int SEG, int ORD, int W, bool PERSIST, bool RING = false>
 __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
                                           uint64_t *__restrict__ out, const StepArgs &a,
-                                          int turns, int tile, int ntx)
+                                          int turns, int tile, int ntx,
+                                          RingArgs ra = RingArgs{})
 {
     constexpr int ND = 2 * W;                            // dwords per lane and row
     constexpr int NS = 2 * ND;                           // row-sum dwords (2 bits per dword)
@@ -180,6 +194,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     while (r < 0) r += M;
     while (r >= M) r -= M;
     uint32_t off = (uint32_t)r * pitch_b + (uint32_t)gx * (8u * W);
+    [[maybe_unused]] const uint32_t off_first = off;     // (RING: the segment's first row)
     const uint32_t lstep = rev ? span - pitch_b : pitch_b;   // (a reversed segment loads upwards)
     const __amdgpu_buffer_rsrc_t rin =
         __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, (int)span, kBufFlags);
@@ -520,7 +535,101 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
         }
     };
     bool gone = false;
-    if constexpr (ORD == 8 || ORD == 9) {
+    if constexpr (RING) {
+        // K1r: ceil(turns / K) blocks of near-equal depth <= K on the tile held in v.  After
+        // block b the TH x TW interior is exact and everything else is stale; the tile stores
+        // its ring's sources -- interior rows within K of its top or bottom edge and its first
+        // and last interior columns -- into u[b % 2] at their board positions, flags them, waits
+        // for its 8 neighbours' flags, and reloads from u[b % 2] what its neighbours stored: the
+        // K rows above and below its interior (halo lanes included) and the two halo lanes.
+        // Lanes and rows further out (a ragged tile's columns past the east halo lane, rows past
+        // the bottom halo) stay stale: their error moves one cell per turn and the refreshed
+        // halo word / K halo rows are as deep as a plain launch's.  Every tile's interior spans
+        // >= K rows (host-checked), so each ring cell comes from one of the 8 neighbours.
+        // Memory: K1p's uncached buffers (no cache maintenance; loads bypass the vector L1).
+        static_assert(PERSIST && W == 1 && ORD != 4 && ORD != 7 && ORD < 8, "K1r: one word per lane");
+        const int THv = min(TH, a.row_hi - y0), TWv = min(TW, nl - x0);
+        const int nty = (a.row_hi - a.row_lo + TH - 1) / TH;
+        const int nblocks = (ra.turns + K - 1) / K, kbase = ra.turns / nblocks,
+                  kextra = ra.turns % nblocks;
+        bool gave_up = false;
+        for (int b = 0; b < nblocks; ++b) {
+            const int kb = kbase + (b < kextra ? 1 : 0);
+            if constexpr (!kPairs) {
+                for (int t = 0; t < kb; ++t) turn(std::integral_constant<int, 0>{}, (t & 1) * 2 * nslot, t);
+            } else {
+                for (int t = 0; t < kb; t += 2) {
+                    turn(std::integral_constant<int, 0>{}, 0, t);
+                    if (t + 1 == kb) break;
+                    turn(std::integral_constant<int, 1>{}, 0, t + 1);
+                }
+            }
+            if (b + 1 == nblocks) break;
+            uint64_t *const X = (b & 1) ? ra.u1 : ra.u0;
+            const __amdgpu_buffer_rsrc_t rx =
+                __builtin_amdgcn_make_buffer_rsrc((void *)X, (short)0, (int)span, kBufFlags);
+            // (the lane's values pass through an empty asm here, so that what the exchange
+            // derives from them -- two predicates per row -- is formed per exchange instead of
+            // hoisted out of the block loop and held in registers across the turns)
+            int ln = lane, thv = THv, twv = TWv, kk = K;
+            uint32_t off0 = off_first;
+            asm volatile("" : "+v"(ln), "+v"(off0), "+s"(thv), "+s"(twv), "+s"(kk));
+            const int gr = ln / C, cl = ln - gr * C;
+            const bool lv = gr < G;
+            const int tr0 = (wave * G + gr) * SEG;       // the lane's first tile row
+            if (lv && cl >= 1 && cl <= twv) {
+                const bool side = cl == 1 || cl == twv;
+                uint32_t so = off0;
+#pragma unroll
+                for (int i = 0; i < SEG; ++i) {
+                    const int j = tr0 + i - kk;           // interior row of the tile
+                    if (j >= 0 && j < thv && (side || j < kk || j >= thv - kk))
+                        buf_store(v[i], rx, so, 0);
+                    so += pitch_b;
+                    so = so >= span ? so - span : so;
+                }
+            }
+            __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));   // this wave's stores are done
+            __syncthreads();                                     // ... and every wave's
+            // (u0 / u1 are uncached: completed stores are in memory, visible to every XCD)
+            if (threadIdx.x == 0) {
+                __hip_atomic_store(ra.flags + tile, ra.epoch + (unsigned)b + 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (threadIdx.x < 8) {                       // one neighbour per lane 0..7
+                const int jn = (int)threadIdx.x + (threadIdx.x >= 4 ? 1 : 0);   // skip (0, 0)
+                const int ny = (ty + jn / 3 - 1 + nty) % nty, nx = (tx + jn % 3 - 1 + ntx) % ntx;
+                const unsigned want = ra.epoch + (unsigned)b + 1u;
+                const unsigned *f = ra.flags + ny * ntx + nx;
+                bool seen = false;
+                for (int spin = 0; !seen && spin < GOL_TILE_SPIN_LIMIT; ++spin) {
+                    const unsigned fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    seen = (int)(fv - want) >= 0;
+                    if (!seen) __builtin_amdgcn_s_sleep(1);
+                }
+                gave_up |= !seen;
+            }
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __syncthreads();
+            if (lv) {
+                const bool hl = cl == 0 || cl == twv + 1;
+                uint32_t lo = off0;
+#pragma unroll
+                for (int i = 0; i < SEG; ++i) {
+                    const int tr = tr0 + i;
+                    if (tr < 2 * kk + thv && (hl || tr < kk || tr >= kk + thv)) {
+                        const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(rx, lo, 0, kLoadAux);
+                        v[i][0] = w.x;
+                        v[i][1] = w.y;
+                    }
+                    lo += pitch_b;
+                    lo = lo >= span ? lo - span : lo;
+                }
+            }
+        }
+        if (gave_up && a.err)
+            __hip_atomic_store(a.err, kDevErrTileFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if constexpr (ORD == 8 || ORD == 9) {
         // ORD 8: ORD 5's turn as one inline-asm block with a hand-made VGPR assignment
         // (gol_tile_turn.h, generated by gen_tile_turn.py: every v_bitop3 reads registers of
         // both parities, which the compiler's allocation does not ensure -- a v_bitop3 whose
@@ -884,9 +993,6 @@ __global__ __launch_bounds__(1024, 1) void k_step_tile_pair(const uint64_t *__re
 // are there -- which also means they finished reading the buffer it is about to overwrite.
 // A wait that gives up after kTileSpinLimit polls marks the error word (GOL_EHIP at the next
 // synchronising call) and goes on with a wrong board rather than hang.
-#ifndef GOL_TILE_SPIN_LIMIT
-#define GOL_TILE_SPIN_LIMIT (1 << 22)
-#endif
 template <int SEG, int ORD, int W>
 __global__ __launch_bounds__(1024, 1) void k_tile_persist(
     const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t *u0, uint64_t *u1,
@@ -937,6 +1043,20 @@ __global__ __launch_bounds__(1024, 1) void k_tile_persist(
         __hip_atomic_store(a.err, kDevErrTileFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+
+// K1r k_tile_ring: K1p's resident tiles without the round trip of the whole tile -- between
+// blocks a tile stores and reloads only its ring (tile_pass RING).  Small torus boards: every
+// tile one resident workgroup (host-checked: a wait for a tile that never runs gives up after
+// GOL_TILE_SPIN_LIMIT polls and marks the error word).  u0 / u1: uncached board-layout buffers.
+template <int SEG, int ORD>
+__global__ __launch_bounds__(1024, 1) void k_tile_ring(
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t *u0, uint64_t *u1,
+    StepArgs a, int turns, int K, int ntx, int ntiles, unsigned *flags, unsigned epoch)
+{
+    const int tile = tile_of_block(ntiles);
+    if (tile >= ntiles) return;                          // (never waited for)
+    tile_pass<SEG, ORD, 1, true, true>(in, out, a, K, tile, ntx, RingArgs{u0, u1, flags, epoch, turns});
+}
 
 // K1q k_tile_stream: K1p's blocks for boards whose tiles do not all fit at once.  One launch
 // runs `turns` turns as blocks of <= K turns; the (block, tile) items are taken in order from

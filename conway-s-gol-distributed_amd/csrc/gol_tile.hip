@@ -73,6 +73,30 @@ static void *persist_fn(int code)
 #endif
 }
 
+// k_tile_ring instantiations (K1r, small torus boards): the C2 / C3 shape families
+static void *ring_fn(int code)
+{
+    static_assert(std::size(kTileRingCodes) == 10, "ring_fn covers kTileRingCodes");
+#if GOL_TOOLS
+    switch (code) {
+    case 103: return reinterpret_cast<void *>(&k_tile_ring<3, 1>);
+    case 203: return reinterpret_cast<void *>(&k_tile_ring<3, 2>);
+    case 503: return reinterpret_cast<void *>(&k_tile_ring<3, 5>);
+    case 504: return reinterpret_cast<void *>(&k_tile_ring<4, 5>);
+    case 506: return reinterpret_cast<void *>(&k_tile_ring<6, 5>);
+    case 508: return reinterpret_cast<void *>(&k_tile_ring<8, 5>);
+    case 512: return reinterpret_cast<void *>(&k_tile_ring<12, 5>);
+    case 516: return reinterpret_cast<void *>(&k_tile_ring<16, 5>);
+    case 112: return reinterpret_cast<void *>(&k_tile_ring<12, 1>);
+    case 116: return reinterpret_cast<void *>(&k_tile_ring<16, 1>);
+    default: return nullptr;
+    }
+#else
+    (void)code;
+    return nullptr;
+#endif
+}
+
 // ORD 6 (the barrier after the interior rows, edge sums read back): the 6-8 waves per SIMD
 // segments only
 static void *tile_fn6(int seg)
@@ -280,6 +304,45 @@ hipError_t launch_tile_persist(const StepArgs &a, int turns, int K, uint64_t *u0
 }  // namespace golk
 
 namespace golk {
+
+bool tile_ring_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg, int ncu)
+{
+    void *fn = ring_fn(seg);
+    if (!fn || !tile_shape_ok(nw, K, tile_h, tile_w, seg) || ncu < 1) return false;
+    const int nty = (rows + tile_h - 1) / tile_h;
+    const int last_h = rows - (nty - 1) * tile_h;
+    // a tile's ring comes from its 8 neighbours only: K rows within every tile's interior
+    if (K > tile_h || K > last_h) return false;
+    const long long ntiles = tile_count(nw, rows, tile_h, tile_w, seg);
+    const long long blocks = (ntiles + 7) / 8 * 8;
+    const int threads = 64 * tile_waves(K, tile_h, tile_w, seg);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads,
+                                                     tile_lds_bytes_code(threads, seg)) != hipSuccess)
+        return false;
+    return per_cu > 0 && blocks <= (long long)ncu * per_cu;   // every tile resident at once
+}
+
+hipError_t launch_tile_ring(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
+                            unsigned *flags, unsigned epoch, hipStream_t s)
+{
+    const int rows = a.row_hi - a.row_lo;
+    void *fn = ring_fn(a.tile_seg);
+    if (!fn || !tile_shape_ok(a.nw, K, a.band, a.tile_w, a.tile_seg) || K > rows || turns < 1)
+        return hipErrorInvalidValue;
+    const int ntx = (a.nw + a.tile_w - 1) / a.tile_w;
+    const long long ntiles = (long long)ntx * ((rows + a.band - 1) / a.band);
+    if (ntiles <= 0 || ntiles > (1 << 20)) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)((ntiles + 7) / 8 * 8);
+    const int threads = 64 * tile_waves(K, a.band, a.tile_w, a.tile_seg);
+    StepArgs args = a;
+    const uint64_t *in = a.in;
+    uint64_t *out = a.out;
+    int t = turns, k = K, ntx_arg = ntx, nt = (int)ntiles;
+    void *params[] = {&in, &out, &u0, &u1, &args, &t, &k, &ntx_arg, &nt, &flags, &epoch};
+    return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params,
+                           tile_lds_bytes_code(threads, a.tile_seg), s);
+}
 
 bool tile_stream_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg)
 {

@@ -40,6 +40,10 @@ TILE_STREAM_CODES = (106, 506, 512, 524) if TOOLS_LIB else ()
 TILE_PERSIST_CODES = (102, 103, 104, 106, 108, 112, 116, 403, 404, 406, 408, 412, 416,
                       2, 3, 4, 6, 8, 503, 504, 506, 508) if TOOLS_LIB else ()
 
+# the codes the ring-exchange tile kernel (K1r, round 6) runs (gol_tile.hip ring_fn): tools
+# build only (it measured slower than plain launches, DESIGN.md "K1r")
+TILE_RING_CODES = (103, 203, 503, 504, 506, 508, 512, 516, 112, 116) if TOOLS_LIB else ()
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import golden_data as G
-from conftest import TILE_CODES, TILE_PERSIST_CODES, TILE_STREAM_CODES, tools_only
+from conftest import TILE_CODES, TILE_PERSIST_CODES, TILE_RING_CODES, TILE_STREAM_CODES, tools_only
 
 pytestmark = pytest.mark.gpu
 
@@ -882,6 +882,33 @@ def test_tile_persist_pinned(gol, oracle, monkeypatch, code, shape):
         assert [v for _, v, _ in plan] == [16] and plan[0][0] == turns, plan
         t = e.last_launch_tiles(blocks=True)[0]
         assert (t[0], t[1], t[3]) == (tw, code, K), t
+        mid = e.read_packed()
+        e.step(turns + 3)
+        got = e.read_packed()
+    want = oracle.bit_run(start, w, turns)
+    assert np.array_equal(mid, want)
+    assert np.array_equal(got, oracle.bit_run(want, w, turns + 3))
+
+
+@pytest.mark.parametrize("code", TILE_RING_CODES)
+@pytest.mark.parametrize("shape", range(len(PERSIST_SHAPES)))
+def test_tile_ring_pinned(gol, oracle, monkeypatch, code, shape):
+    """K1r k_tile_ring (K1p's resident tiles kept in registers across blocks; between blocks
+    only each tile's ring passes through memory) for every instantiation it has, on K1p's
+    ragged and self-neighbour shapes, against the oracle; a second call continues."""
+    w, h, tw, th, K, turns = PERSIST_SHAPES[shape]
+    if code % 100 * (64 // (tw + 2)) * 16 < th + 2 * K:
+        pytest.skip("tile taller than 16 waves of this segment")
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+    monkeypatch.setenv("GOL_TILE", f"{tw},{code}")
+    monkeypatch.setenv("GOL_PERSIST", str(K))
+    monkeypatch.setenv("GOL_RING", "1")
+    start = oracle.gen_random(code * 7 + shape, w, h)
+    with _engine(gol, w, h, band_rows=th, turns_per_launch=K) as e:
+        e.load_packed(start)
+        e.step(turns)
+        plan = e.last_launches()
+        assert [v for _, v, _ in plan] == [16] and plan[0][0] == turns, plan
         mid = e.read_packed()
         e.step(turns + 3)
         got = e.read_packed()

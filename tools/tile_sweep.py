@@ -2,7 +2,9 @@
 """k_step_tile shape sweep (K1t): time `--turns` turns per shape, interleaved rounds, HIP
 events on one stream, and check every shape computed the same board.
 usage: python tools/tile_sweep.py --size 5120 --shapes 10:160:4:32,10:80:4:16 [--auto]
-       shape = tile_w:tile_h:seg:K ; --auto adds the engine's own autotuned pick"""
+       shape = tile_w:tile_h:seg:K[:p|:r] ; --auto adds the engine's own autotuned pick;
+       :p = K1p resident tiles (GOL_PERSIST=K), :r = K1r ring exchange (GOL_PERSIST=K GOL_RING=1),
+       both tools build only (GOL_AMD_LIB=.../libgolamd_tools.so)"""
 import argparse
 import json
 import os
@@ -44,11 +46,19 @@ def main():
     stream = torch.cuda.Stream()
     engines = {}
     for sh in [x for x in a.shapes.split(",") if x]:
-        tw, th, seg, K = (int(v) for v in sh.split(":"))
+        parts = sh.split(":")
+        tw, th, seg, K = (int(v) for v in parts[:4])
+        mode = parts[4] if len(parts) > 4 else ""
         os.environ["GOL_MULTI_VARIANT"] = "15"
         os.environ["GOL_TILE"] = f"{tw},{seg}"
+        if mode in ("p", "r"):
+            os.environ["GOL_PERSIST"] = str(K)
+        if mode == "r":
+            os.environ["GOL_RING"] = "1"
         e = gol.Engine(W, H, device=0, band_rows=th, turns_per_launch=K)
         engines[sh] = e
+        os.environ.pop("GOL_PERSIST", None)
+        os.environ.pop("GOL_RING", None)
     os.environ.pop("GOL_MULTI_VARIANT", None)
     os.environ.pop("GOL_TILE", None)
     if a.auto:
