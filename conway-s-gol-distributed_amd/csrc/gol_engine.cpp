@@ -572,8 +572,14 @@ hipError_t persist_launch(gol_ctx *c, golk::StepArgs a, int turns, int K)
     const unsigned nblocks = (unsigned)((turns + K - 1) / K);
     const unsigned epoch = c->pepoch + 1;
     c->pepoch = epoch + nblocks;
-    if (c->persist_ring)                     // K1r: only the rings pass through u0 / u1
-        return golk::launch_tile_ring(a, turns, K, c->pu[0], c->pu[1], c->pflags, epoch, c->stream);
+    if (c->persist_ring) {                   // K1r: only the rings pass through u0 / u1
+        // (GOL_RING=2, experiments: a grid-wide barrier per block on K1q's counter)
+        const bool grid = getenv("GOL_RING") && atoi(getenv("GOL_RING")) == 2;
+        const unsigned base = c->pcount;
+        if (grid) c->pcount += (unsigned)ntiles * (nblocks - 1);
+        return golk::launch_tile_ring(a, turns, K, c->pu[0], c->pu[1], c->pflags, epoch,
+                                      grid ? c->pcounter : nullptr, base, c->stream);
+    }
     return golk::launch_tile_persist(a, turns, K, c->pu[0], c->pu[1], c->pflags, epoch, c->stream);
 }
 

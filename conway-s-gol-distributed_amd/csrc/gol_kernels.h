@@ -253,8 +253,11 @@ hipError_t launch_tile_stream(const StepArgs &a, int turns, int K, uint64_t *u0,
 // K1r k_tile_ring (gol_tile.h): K1p's contract (flags, epoch) with the tiles kept in registers
 // across blocks; only their rings pass through u0 / u1 (uncached, board-sized).
 bool tile_ring_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg, int ncu);
+// gcount (tools experiments, else nullptr): a grid-wide barrier per block on that counter,
+// whose value at the launch is gbase (it advances by tiles x (blocks - 1))
 hipError_t launch_tile_ring(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
-                            unsigned *flags, unsigned epoch, hipStream_t s);
+                            unsigned *flags, unsigned epoch, unsigned *gcount, unsigned gbase,
+                            hipStream_t s);
 int auto_band(int width, int rows);
 hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s);
 

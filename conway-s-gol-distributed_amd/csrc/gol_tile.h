@@ -143,6 +143,10 @@ struct RingArgs {
     unsigned *flags;            // per tile: epoch + b + 1 once its block-b edges are stored
     unsigned epoch;
     int turns;                  // turns of the launch, in blocks of <= K
+    unsigned *gcount;           // (tools, GOL_RING=2) non-null: a grid-wide barrier per block
+    unsigned gbase;             // instead of the 8 neighbours: *gcount at the launch's start
+    int ablate;                 // (tools timing ablations, wrong boards: 1 no edge stores, 2 no
+                                // flag wait, 4 no ring loads)
 };
 template <int SEG, int ORD, int W, bool PERSIST, bool RING = false>
 __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
@@ -577,7 +581,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             const int gr = ln / C, cl = ln - gr * C;
             const bool lv = gr < G;
             const int tr0 = (wave * G + gr) * SEG;       // the lane's first tile row
-            if (lv && cl >= 1 && cl <= twv) {
+            if (lv && cl >= 1 && cl <= twv && !(ra.ablate & 1)) {
                 const bool side = cl == 1 || cl == twv;
                 uint32_t so = off0;
 #pragma unroll
@@ -596,7 +600,18 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
                 __hip_atomic_store(ra.flags + tile, ra.epoch + (unsigned)b + 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (threadIdx.x < 8) {                       // one neighbour per lane 0..7
+            if (ra.gcount && threadIdx.x == 0) {        // (every tile: a grid-wide barrier)
+                __hip_atomic_fetch_add(ra.gcount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned want = ra.gbase + (unsigned)(b + 1) * (unsigned)(nty * ntx);
+                bool seen = false;
+                for (int spin = 0; !seen && spin < GOL_TILE_SPIN_LIMIT; ++spin) {
+                    const unsigned fv = __hip_atomic_load(ra.gcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    seen = (int)(fv - want) >= 0;
+                    if (!seen) __builtin_amdgcn_s_sleep(1);
+                }
+                gave_up |= !seen;
+            }
+            if (!ra.gcount && threadIdx.x < 8 && !(ra.ablate & 2)) {   // one neighbour per lane 0..7
                 const int jn = (int)threadIdx.x + (threadIdx.x >= 4 ? 1 : 0);   // skip (0, 0)
                 const int ny = (ty + jn / 3 - 1 + nty) % nty, nx = (tx + jn % 3 - 1 + ntx) % ntx;
                 const unsigned want = ra.epoch + (unsigned)b + 1u;
@@ -611,7 +626,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
             }
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             __syncthreads();
-            if (lv) {
+            if (lv && !(ra.ablate & 4)) {
                 const bool hl = cl == 0 || cl == twv + 1;
                 uint32_t lo = off0;
 #pragma unroll
@@ -1051,11 +1066,13 @@ __global__ __launch_bounds__(1024, 1) void k_tile_persist(
 template <int SEG, int ORD>
 __global__ __launch_bounds__(1024, 1) void k_tile_ring(
     const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t *u0, uint64_t *u1,
-    StepArgs a, int turns, int K, int ntx, int ntiles, unsigned *flags, unsigned epoch)
+    StepArgs a, int turns, int K, int ntx, int ntiles, unsigned *flags, unsigned epoch,
+    unsigned *gcount, unsigned gbase, int ablate)
 {
     const int tile = tile_of_block(ntiles);
     if (tile >= ntiles) return;                          // (never waited for)
-    tile_pass<SEG, ORD, 1, true, true>(in, out, a, K, tile, ntx, RingArgs{u0, u1, flags, epoch, turns});
+    tile_pass<SEG, ORD, 1, true, true>(in, out, a, K, tile, ntx,
+                                       RingArgs{u0, u1, flags, epoch, turns, gcount, gbase, ablate});
 }
 
 // K1q k_tile_stream: K1p's blocks for boards whose tiles do not all fit at once.  One launch

@@ -324,7 +324,8 @@ bool tile_ring_ok(int nw, int rows, int K, int tile_h, int tile_w, int seg, int 
 }
 
 hipError_t launch_tile_ring(const StepArgs &a, int turns, int K, uint64_t *u0, uint64_t *u1,
-                            unsigned *flags, unsigned epoch, hipStream_t s)
+                            unsigned *flags, unsigned epoch, unsigned *gcount, unsigned gbase,
+                            hipStream_t s)
 {
     const int rows = a.row_hi - a.row_lo;
     void *fn = ring_fn(a.tile_seg);
@@ -339,7 +340,9 @@ hipError_t launch_tile_ring(const StepArgs &a, int turns, int K, uint64_t *u0, u
     const uint64_t *in = a.in;
     uint64_t *out = a.out;
     int t = turns, k = K, ntx_arg = ntx, nt = (int)ntiles;
-    void *params[] = {&in, &out, &u0, &u1, &args, &t, &k, &ntx_arg, &nt, &flags, &epoch};
+    int ablate = getenv("GOL_RING_ABLATE") ? atoi(getenv("GOL_RING_ABLATE")) : 0;   // (tools timing)
+    void *params[] = {&in, &out, &u0, &u1, &args, &t, &k, &ntx_arg, &nt, &flags, &epoch,
+                      &gcount, &gbase, &ablate};
     return hipLaunchKernel(fn, dim3(blocks), dim3(threads), params,
                            tile_lds_bytes_code(threads, a.tile_seg), s);
 }

@@ -3,7 +3,8 @@
 events on one stream, and check every shape computed the same board.
 usage: python tools/tile_sweep.py --size 5120 --shapes 10:160:4:32,10:80:4:16 [--auto]
        shape = tile_w:tile_h:seg:K[:p|:r] ; --auto adds the engine's own autotuned pick;
-       :p = K1p resident tiles (GOL_PERSIST=K), :r = K1r ring exchange (GOL_PERSIST=K GOL_RING=1),
+       :p = K1p resident tiles (GOL_PERSIST=K), :r = K1r ring exchange (GOL_PERSIST=K GOL_RING=1), :g = K1r with a
+       grid-wide barrier per block (GOL_RING=2),
        both tools build only (GOL_AMD_LIB=.../libgolamd_tools.so)"""
 import argparse
 import json
@@ -51,10 +52,10 @@ def main():
         mode = parts[4] if len(parts) > 4 else ""
         os.environ["GOL_MULTI_VARIANT"] = "15"
         os.environ["GOL_TILE"] = f"{tw},{seg}"
-        if mode in ("p", "r"):
+        if mode in ("p", "r", "g"):
             os.environ["GOL_PERSIST"] = str(K)
-        if mode == "r":
-            os.environ["GOL_RING"] = "1"
+        if mode in ("r", "g"):
+            os.environ["GOL_RING"] = "1" if mode == "r" else "2"
         e = gol.Engine(W, H, device=0, band_rows=th, turns_per_launch=K)
         engines[sh] = e
         os.environ.pop("GOL_PERSIST", None)
