@@ -998,12 +998,12 @@ constexpr KnownShape kKnownShapes[] = {
     // 115.9-118.4k for round 5's K = 24 on 30 x 336 8-wave tiles (alternating on one box; 1000
     // turns 126.8k against 125.8k; K = 24 on 30 x 528 12-wave tiles: 112k)
     {65536, 65536, {20, 472, 30, 516, 0}, 33.6f},
-    // configs[2]: ORD 5, SEG 16, 8-wave workgroups, 14 x 448 tiles: 2.85 us per turn, the
-    // fastest of 36 K = 32 shapes, and in the bench 94.8-95.0k against 94.0-94.2k for round 5's
-    // 14 x 320 ORD 1 SEG 12 (alternating, profiles/r06_headline_pin_ab.log; that one had beaten
-    // round 4's ORD 1 SEG 6 16-wave pick, 2.84-2.92 against 3.06-3.20 us per turn,
-    // profiles/r05_c3_codes_ab.log)
-    {16384, 16384, {32, 448, 14, 516, 0}, 2.85f},
+    // configs[2]: ORD 5, SEG 16, 8-wave workgroups, 14 x 416 tiles, K = 48 (deeper than the
+    // planner's tables: k_step_tile runs up to 64 turns): 760 tiles, at most 3 per CU, 2.73-2.74
+    // us per turn against 2.83-2.84 for round 6's first pin, 14 x 448 at K = 32 (703 tiles),
+    // which was the fastest of 36 K = 32 shapes (profiles/r06_c3_deep_k.log; before it round
+    // 5's 14 x 320 ORD 1 SEG 12, profiles/r06_headline_pin_ab.log)
+    {16384, 16384, {48, 416, 14, 516, 0}, 2.74f},
     // configs[1]: ORD 2, SEG 3, 16-wave workgroups; 0.57-0.59 us per turn (BENCH_r04)
     {5120, 5120, {32, 128, 14, 203, 0}, 0.58f},
     // configs[3..4] as row strips with 128-row halos (buffer = H / N + 256 rows):
@@ -1854,8 +1854,9 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     const bool pinned = getenv("GOL_MULTI_VARIANT") != nullptr;
     if (c->fast && c->tpl > 1 &&
         ((small && !pinned && cfg->band_rows <= 0) || c->multi_variant == golk::kMultiTile)) {
-        int K = cfg->turns_per_launch > 0 ? std::min(cfg->turns_per_launch, 32) : 0;
-        if (const char *v = getenv("GOL_TURNS_PER_LAUNCH")) K = std::max(2, std::min(atoi(v), 32));
+        int K = cfg->turns_per_launch > 0 ? std::min(cfg->turns_per_launch, golk::kMaxTileTurns) : 0;
+        if (const char *v = getenv("GOL_TURNS_PER_LAUNCH"))
+            K = std::max(2, std::min(atoi(v), golk::kMaxTileTurns));
         std::vector<TileShape> cand = tile_candidates(c->ncu, c->nw, c->buf_rows, 1 << 20);
         for (const TileShape &t : cand)
             if (K == 0 || t.K == K) {

@@ -129,6 +129,10 @@ bool fast_path_ok(int width);
 // turns, reading rows [row_lo - turns, row_hi + turns) (mod modrows).  No blocked mask,
 // no counts.  turns in 2 .. multi_max_turns(variant).
 constexpr int kMaxTurnsPerLaunch = 32;
+// k_step_tile alone goes deeper: its halo word (64 cells) and K halo rows stay exact up to 64
+// turns (the planner's per-depth tables stop at kMaxTurnsPerLaunch; deeper K1t launches are
+// pinned or requested, never searched)
+constexpr int kMaxTileTurns = 64;
 // 32 for the helix k_step_wg variants, 16 for band-tiled k_step_wg, 8..12 for k_step_skew
 int multi_max_turns(int variant);
 // k_step_wg on helix tiles: wavefronts per workgroup at depth `turns` -- 4 up to K = 16, then

@@ -618,7 +618,7 @@ hipError_t launch_step(const StepArgs &a, bool fast, hipStream_t s)
 
 int multi_max_turns(int variant)
 {
-    if (variant == kMultiTile) return kMaxTurnsPerLaunch;
+    if (variant == kMultiTile) return kMaxTileTurns;
     if (variant == kMultiWgHx || variant == kMultiWgPg) return GOL_TOOLS ? kWgDeepMax : 16;
     if (variant == kMultiWgHxS || variant == kMultiWgPgS) return 16;
     return is_wg_variant(variant) ? 16 : variant == kMultiSkewILW16 ? 12 : 8;
