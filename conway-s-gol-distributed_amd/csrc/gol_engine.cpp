@@ -79,6 +79,9 @@ struct gol_ctx {
     int multi_variant = golk::kMultiSkewILW16;  // temporal-blocking kernel (kMulti*)
     int band_multi = 64;                     // band height of the multi-turn kernel (depth tpl)
     int band_at[golk::kMaxTurnsPerLaunch + 1] = {};   // band_for_depth cache (0 = not yet)
+    // a pinned k_step_tile shape's tile height for launches of depth <= short_k (0: none): a
+    // short step's one shallow launch takes the taller tile its depth allows
+    int short_k = 0, short_band = 0;
     // launch planner (autotuned engines): plan[t] = the first launch of the fastest measured
     // sequence of launches for t turns (t <= kPlanMax; k = 0: no plan, use the even split)
     std::vector<Launch> plan;
@@ -398,6 +401,9 @@ int band_same_rounds(const gol_ctx *c, int var, int K0, int band0, int k)
 // (gol_config.band_rows) is kept
 int band_for_depth(gol_ctx *c, int k)
 {
+    if (c->short_k > 0 && c->multi_variant == golk::kMultiTile && c->cfg.band_rows <= 0 &&
+        k >= 2 && k <= c->short_k)
+        return c->short_band;
     if (k == c->tpl || c->cfg.band_rows > 0 || k < 2 || k > golk::kMaxTurnsPerLaunch)
         return c->band_multi;
     int &b = c->band_at[k];
@@ -711,6 +717,7 @@ void apply_tile(gol_ctx *c, const TileShape &t)
     c->band_multi = t.th;
     c->tile_w = t.tw;
     c->tile_seg = t.seg;
+    c->short_k = c->short_band = 0;
     for (int &b : c->band_at) b = 0;
     c->plan.clear();
     c->seq.clear();
@@ -986,18 +993,20 @@ struct KnownShape {
     int width, rows;
     TileShape t;                             // K, tile height, tile width (lanes), segment code
     float us_per_turn;                       // measured steady state (round-4 sweeps)
+    int short_K = 0, short_th = 0;           // launches of depth <= short_K: tiles short_th tall
 };
 constexpr KnownShape kKnownShapes[] = {
 #ifdef GOL_PIN_OVERRIDE   // (A/B builds: an entry ahead of the table, e.g. 65536,65536,{20,472,30,516,0},34.f)
     {GOL_PIN_OVERRIDE},
 #endif
-    // configs[3..4]: K = 20 (the driver's 20-turn call is one launch of exactly this depth) on
-    // 30 x 472 tiles of ORD 5 SEG 16 in 16-wave workgroups (2 per CU, 8 waves per SIMD): the
-    // fastest of 30 K = 20 shapes (33.6 us per turn; profiles/r06_headline_pin_ab.log) and, in
-    // the bench, 118.3-121.0k against 117.7-119.4k for 30 x 536 SEG 24 12-wave tiles and
-    // 115.9-118.4k for round 5's K = 24 on 30 x 336 8-wave tiles (alternating on one box; 1000
-    // turns 126.8k against 125.8k; K = 24 on 30 x 528 12-wave tiles: 112k)
-    {65536, 65536, {20, 472, 30, 516, 0}, 33.6f},
+    // configs[3..4]: 30-lane tiles of ORD 5 SEG 16 in 16-wave workgroups (2 per CU, 8 waves
+    // per SIMD).  Long steps: K = 30 on 30 x 452 tiles, 33.09-33.12 us per turn against
+    // 33.72-33.75 for K = 20 (profiles/r06_c3_deep_k.log, 65536 sweep).  Launches of <= 20
+    // turns -- the driver's 20-turn call is one launch of exactly 20 -- keep 30 x 472 tiles:
+    // the fastest of 30 K = 20 shapes (33.6 us per turn; profiles/r06_headline_pin_ab.log) and,
+    // in the bench, 118.3-121.0k against 117.7-119.4k for 30 x 536 SEG 24 12-wave tiles and
+    // 115.9-118.4k for round 5's K = 24 on 30 x 336 8-wave tiles (alternating on one box)
+    {65536, 65536, {30, 452, 30, 516, 0}, 33.1f, 20, 472},
     // configs[2]: ORD 5, SEG 16, 8-wave workgroups, 14 x 416 tiles, K = 48 (deeper than the
     // planner's tables: k_step_tile runs up to 64 turns): 760 tiles, at most 3 per CU, 2.73-2.74
     // us per turn against 2.83-2.84 for round 6's first pin, 14 x 448 at K = 32 (703 tiles),
@@ -1926,6 +1935,11 @@ int gol_create_ex(const gol_config *cfg, gol_ctx **out)
     if (tuning && !pinned && cfg->turns_per_launch <= 0 && !getenv("GOL_TILE") &&
         !(at && atoi(at) == 2) && known_shape(c, &ks)) {
         apply_tile(c, ks.t);
+        if (ks.short_K >= 2 && ks.short_K < ks.t.K &&
+            golk::tile_shape_ok(c->nw, ks.short_K, ks.short_th, ks.t.tw, ks.t.seg)) {
+            c->short_k = ks.short_K;
+            c->short_band = ks.short_th;
+        }
         c->tuned_us_per_turn = ks.us_per_turn;
         c->shape_source = 2;
         tuning = false;

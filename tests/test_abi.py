@@ -188,13 +188,17 @@ def test_pinned_shapes_match_the_tests():
                             "gol_engine.cpp")).read()
     body = src[src.index("constexpr KnownShape kKnownShapes[] = {"):]
     body = body[:body.index("};")]
-    got = {(int(w), int(r)): (int(k), int(th), int(tw), int(code)) for w, r, k, th, tw, code in
-           re.findall(r"\{(\d+), (\d+), \{(\d+), (\d+), (\d+), (\d+), 0\}", body)}
+    rows = re.findall(r"\{(\d+), (\d+), \{(\d+), (\d+), (\d+), (\d+), 0\}, [\d.]+f(?:, (\d+), (\d+))?\}",
+                      body)
+    got = {(int(w), int(r)): (int(k), int(th), int(tw), int(code))
+           for w, r, k, th, tw, code, _, _ in rows}
+    short = {int(w): (int(sk), int(sth)) for w, r, _, _, _, _, sk, sth in rows if sk}
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import test_gpu_engine as T
     want = {(s, s): v for s, v in T.PINNED_SHAPES.items()}
     want.update(T.PINNED_STRIP_SHAPES)
     assert got == want
+    assert short == T.PINNED_SHORT
     assert all(v[3] in TILE_CODES for v in got.values())
 
 

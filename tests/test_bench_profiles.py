@@ -69,7 +69,8 @@ def test_pinned_shapes_have_profiles():
     shapes += [(w, _tile_shape(K, th, tw, code, rows))
                for (w, rows), (K, th, tw, code) in T.PINNED_STRIP_SHAPES.items()]
     K, th, tw, code = T.PINNED_SHAPES[65536]
-    shapes.append((65536, _tile_shape(20, th, tw, code, 65536)))
+    ks, ths = T.PINNED_SHORT[65536]
+    shapes.append((65536, _tile_shape(ks, ths, tw, code, 65536)))
     for size, shape in shapes:
         d, src = b.pmc_summary(size, shape["turns"], shape)
         assert d and d["traffic_bytes_per_launch"] > 0, (size, shape)
