@@ -188,6 +188,22 @@ __device__ __forceinline__ void buf_store(const uint32_t (&o)[4], __amdgpu_buffe
     __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, soff, 0);
 }
 
+// (A/B builds: the cache policy of k_step_tile's final stores and first loads, the aux operand
+// of the buffer instruction -- gfx950: 1 = sc0, 2 = nt, 16 = sc1; 0 in the product)
+#ifndef GOL_TILE_STORE_AUX
+#define GOL_TILE_STORE_AUX 0
+#endif
+#ifndef GOL_TILE_LOAD_AUX
+#define GOL_TILE_LOAD_AUX 0
+#endif
+template <int AUX>
+__device__ __forceinline__ void buf_store_aux(const uint32_t (&o)[2], __amdgpu_buffer_rsrc_t r,
+                                              uint32_t voff)
+{
+    const u32x2 d = {o[0], o[1]};
+    __builtin_amdgcn_raw_buffer_store_b64(d, r, voff, 0, AUX);
+}
+
 template <int ND> struct LaneDw;
 template <> struct LaneDw<1> { using T = uint32_t; };
 template <> struct LaneDw<2> { using T = uint2; };

@@ -208,7 +208,7 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
     // PERSIST: loads bypass this CU's vector L1 (sc1): block b reads rows other CUs wrote
     // since block b - 2 left lines of the same buffer in it, and the L1 is never refreshed
     // by another CU's stores
-    constexpr int kLoadAux = PERSIST ? 16 : 0;
+    constexpr int kLoadAux = PERSIST ? 16 : GOL_TILE_LOAD_AUX;
     uint32_t v[SEG][ND];
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
@@ -756,7 +756,12 @@ __device__ __forceinline__ void tile_pass(const uint64_t *__restrict__ in,
 #pragma unroll
     for (int i = 0; i < SEG; ++i) {
         const int tr = t0 + dr * i;
-        if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) buf_store(v[i], rout, so, 0);
+        if (tr >= K && tr < K + TH && y0 - K + tr < a.row_hi) {
+            if constexpr (W == 1 && GOL_TILE_STORE_AUX != 0)
+                buf_store_aux<GOL_TILE_STORE_AUX>(v[i], rout, so);
+            else
+                buf_store(v[i], rout, so, 0);
+        }
         so += sstep;
     }
 }
