@@ -855,6 +855,31 @@ def test_tile_code_pinned(gol, oracle, monkeypatch, code):
     assert np.array_equal(got, oracle.bit_run(start, w, 3 * K - 1))
 
 
+@pytest.mark.parametrize("code,tw,th,K", [(516, 14, 416, 48), (516, 30, 120, 64), (504, 14, 128, 64),
+                                          (203, 14, 60, 64), (112, 30, 100, 33)])
+def test_tile_deep_launches(gol, oracle, monkeypatch, code, tw, th, K):
+    """k_step_tile launches deeper than the planner's tables (33..64 turns, kMaxTileTurns: the
+    one-word halo lanes and K halo rows stay exact to K = 64; 16384^2 is pinned at K = 48,
+    65536^2 at 30) against the oracle on a ragged board (66 words = 4 x 14 + 10 = 2 x 30 + 6
+    lanes; 600 rows, a partial last tile row): one full launch, then 2K - 1 turns as two
+    near-equal launches."""
+    w, h = 4224, 600
+    monkeypatch.setenv("GOL_MULTI_VARIANT", "15")
+    monkeypatch.setenv("GOL_TILE", f"{tw},{code}")
+    start = oracle.gen_random(code + K, w, h)
+    with _engine(gol, w, h, band_rows=th, turns_per_launch=K) as e:
+        assert e.info().turns_per_launch == K
+        e.load_packed(start)
+        e.step(K)
+        assert [x[0] for x in e.last_launches()] == [K]
+        e.step(2 * K - 1)
+        assert sorted(x[0] for x in e.last_launches()) == [K - 1, K]
+        assert {(t[0], t[1], t[3]) for t in e.last_launch_tiles(blocks=True)} == \
+            {(tw, code, K - 1), (tw, code, K)}
+        got = e.read_packed()
+    assert np.array_equal(got, oracle.bit_run(start, w, 3 * K - 1))
+
+
 PERSIST_SHAPES = [
     # (width, height, tile_w, tile_h, K, turns): ragged both ways, several blocks and a short
     # last one, a single tile row / column (a tile is its own neighbour), K == last tile row
