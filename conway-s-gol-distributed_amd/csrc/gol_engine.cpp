@@ -1007,12 +1007,13 @@ constexpr KnownShape kKnownShapes[] = {
     // in the bench, 118.3-121.0k against 117.7-119.4k for 30 x 536 SEG 24 12-wave tiles and
     // 115.9-118.4k for round 5's K = 24 on 30 x 336 8-wave tiles (alternating on one box)
     {65536, 65536, {30, 452, 30, 516, 0}, 33.1f, 20, 472},
-    // configs[2]: ORD 5, SEG 16, 8-wave workgroups, 14 x 416 tiles, K = 48 (deeper than the
-    // planner's tables: k_step_tile runs up to 64 turns): 760 tiles, at most 3 per CU, 2.73-2.74
-    // us per turn against 2.83-2.84 for round 6's first pin, 14 x 448 at K = 32 (703 tiles),
-    // which was the fastest of 36 K = 32 shapes (profiles/r06_c3_deep_k.log; before it round
-    // 5's 14 x 320 ORD 1 SEG 12, profiles/r06_headline_pin_ab.log)
-    {16384, 16384, {48, 416, 14, 516, 0}, 2.74f},
+    // configs[2]: ORD 5, SEG 16, 8-wave workgroups, 14 x 410 tiles, K = 51 (deeper than the
+    // planner's tables: k_step_tile runs up to 64 turns): 760 tiles, at most 3 per CU, 2.726-2.730
+    // us per turn against 2.742 for K = 48 on 14 x 416 and 2.83-2.84 for round 6's first pin,
+    // 14 x 448 at K = 32 (703 tiles), which was the fastest of 36 K = 32 shapes
+    // (profiles/r06_c3_deep_k.log; before it round 5's 14 x 320 ORD 1 SEG 12,
+    // profiles/r06_headline_pin_ab.log)
+    {16384, 16384, {51, 410, 14, 516, 0}, 2.73f},
     // configs[1]: ORD 2, SEG 3, 16-wave workgroups; 0.57-0.59 us per turn (BENCH_r04)
     {5120, 5120, {32, 128, 14, 203, 0}, 0.58f},
     // configs[3..4] as row strips with 128-row halos (buffer = H / N + 256 rows):
