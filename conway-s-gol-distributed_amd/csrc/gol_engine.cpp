@@ -1014,8 +1014,11 @@ constexpr KnownShape kKnownShapes[] = {
     // (profiles/r06_c3_deep_k.log; before it round 5's 14 x 320 ORD 1 SEG 12,
     // profiles/r06_headline_pin_ab.log)
     {16384, 16384, {51, 410, 14, 516, 0}, 2.73f},
-    // configs[1]: ORD 2, SEG 3, 16-wave workgroups; 0.57-0.59 us per turn (BENCH_r04)
-    {5120, 5120, {32, 128, 14, 203, 0}, 0.58f},
+    // configs[1]: ORD 2, SEG 3, 16-wave workgroups of 10-lane tiles (5 groups per wave), 10 x
+    // 160 at K = 40: 8 x 32 = 256 tiles, one per CU with none idle (80 words = 8 x 10 exactly),
+    // 0.524-0.530 us per turn against 0.550-0.553 for the earlier 14 x 128 at K = 32 (240
+    // tiles; profiles/r06_c3_deep_k.log, C2 section)
+    {5120, 5120, {40, 160, 10, 203, 0}, 0.53f},
     // configs[3..4] as row strips with 128-row halos (buffer = H / N + 256 rows):
     // N = 8 ORD 1 SEG 12 (west carry) on 14 x 352 tiles, 8 launches of 16 turns per window
     // (5.44-5.46 us per turn against 5.69-5.70 for ORD 5 SEG 12 on the same tiles,

@@ -575,7 +575,7 @@ def test_halo_wave_tiles_full_size(gol, monkeypatch, K, key, code):
 # the pinned MI355X launch shapes (gol_engine.cpp kKnownShapes): board -> (K, tile height, tile
 # width in lanes, segment code); the bench's configs run exactly these, and profiles/ has a
 # kernel-trace + PMC summary of each
-PINNED_SHAPES = {65536: (30, 452, 30, 516), 16384: (51, 410, 14, 516), 5120: (32, 128, 14, 203)}
+PINNED_SHAPES = {65536: (30, 452, 30, 516), 16384: (51, 410, 14, 516), 5120: (40, 160, 10, 203)}
 # ... and a pinned shape's tile height for launches of at most K' turns (board -> (K', height)):
 # 65536^2's 20-turn steps (the driver's command) run one K = 20 launch on 472-row tiles
 PINNED_SHORT = {65536: (20, 472)}
@@ -598,8 +598,8 @@ def test_pinned_shape_digest(gol, key):
     full-size digest -- the shapes of PINNED_SHAPES: 65536^2 x 1000 (configs[3], K = 30 on
     30 x 452 tiles of ORD 5 SEG 16 in 16-wave workgroups: 34 launches of 29-30 turns), 16384^2 x 10000
     (configs[2], K = 51 on 14 x 410 tiles of ORD 5 SEG 16: 197 launches of 50-51 turns, deeper
-    than the planner's own tables), 5120^2 x 1000 (configs[1], K = 32
-    on 14 x 128 tiles of ORD 2 SEG 3)."""
+    than the planner's own tables), 5120^2 x 1000 (configs[1], K = 40
+    on 10 x 160 tiles of ORD 2 SEG 3: 256 tiles, 25 launches)."""
     d = _digests()[key]
     K, th, tw, code = PINNED_SHAPES[d["width"]]
     with _engine(gol, d["width"], d["height"]) as e:
